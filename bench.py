@@ -1,0 +1,236 @@
+"""bench.py — headline benchmark (BASELINE.json metric, config 4).
+
+One step = one frame: 1920x1080 x 8 spp x max_depth 4 over the synthetic
+1M-triangle sphere field, rendered by the HIP wavefront path tracer (exactly
+8 x PTPass::OnRun of the reference), i.e. BVH traversal + shading of every
+primary, extension and shadow ray.  The BVH build is done once before the
+timed region (reported separately as build_ms, like the reference's
+GAS/IAS build in PTPass::SetScene).
+
+Multi-GPU (torchrun, one process per GPU): image tiles (32x32) are dealt
+round-robin over ranks (tile t -> rank t % N), each rank renders its tiles,
+and per frame the compact tile radiance is gathered to rank 0 over RCCL and
+scattered into the full image.  Total work is fixed -> "scaling": "strong".
+
+value = Mrays/s over the whole job = (primary + extension + shadow rays of
+all ranks) / (max over ranks of the frame time).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--spheres", type=int, default=500, help="500 -> 1,000,004 triangles (config 4)")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--max-depth", type=int, default=4)
+    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1 only)")
+    ap.add_argument("--cpu-sample-stride", type=int, default=16, help="CPU baseline renders every k-th pixel")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--save", default="", help="write the frame as PNG (rank 0)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device(f"cuda:{local_rank}")
+
+    from pupiloptixlab_amd import scenes
+    from pupiloptixlab_amd.pt_pass import PTPass, FINAL_RESULT
+
+    scene = scenes.sphere_field(args.spheres, args.width, args.height, args.max_depth, seed=1)
+    desc = scene.desc()
+    tris = sum(desc.shapes[i].num_faces for i in range(desc.num_shapes) if desc.shapes[i].kind == 0)
+    n_prims = 0
+    for i in range(desc.num_instances):
+        s = desc.shapes[desc.instances[i].shape]
+        n_prims += 1 if s.kind == 1 else s.num_faces
+
+    pt = PTPass(device=local_rank)
+    pt.set_scene(desc)
+    if world > 1:
+        pt.set_tiling(args.tile, rank, world)
+    n_local = pt.local_pixel_count() if world > 1 else args.width * args.height
+    stream = torch.cuda.current_stream(dev)
+
+    # gather plumbing (rank 0 assembles the frame)
+    if world > 1:
+        counts = [0] * world
+        maps = []
+        for r in range(world):
+            import ctypes as C
+
+            n = C.c_uint32(0)
+            pt._lib.pupil_pt_local_pixels(args.width, args.height, args.tile, r, world, None, C.byref(n))
+            counts[r] = n.value
+            arr = np.zeros(n.value, np.uint32)
+            pt._lib.pupil_pt_local_pixels(args.width, args.height, args.tile, r, world,
+                                          arr.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(n))
+            maps.append(torch.from_numpy(arr.astype(np.int64)).to(dev))
+        max_local = max(counts)
+        send = torch.zeros((max_local, 4), dtype=torch.float32, device=dev)
+        recv = [torch.zeros_like(send) for _ in range(world)] if rank == 0 else None
+        full = torch.zeros((args.width * args.height, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+
+    def frame():
+        pt.mark_dirty()  # each step is a fresh 8-spp frame from seed 0
+        pt.render(args.spp, stream=stream)
+        if world > 1:
+            send[:n_local].copy_(pt.buffers.get(FINAL_RESULT))
+            dist.gather(send, recv, dst=0)
+            if rank == 0:
+                for r in range(world):
+                    full.index_copy_(0, maps[r], recv[r][: counts[r]])
+
+    # one instrumented frame for the traversal byte counts (untimed)
+    pt.mark_dirty()
+    pt.render(args.spp, collect_stats=True, stream=stream)
+    torch.cuda.synchronize(dev)
+    st_bytes = pt.stats()
+
+    for _ in range(args.warmup):
+        frame()
+    torch.cuda.synchronize(dev)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    trace_ms = 0.0
+    trace_launches = 0
+    rays_local = 0
+    for _ in range(args.steps):
+        frame()
+        st = pt.stats()  # waits for the frame's end event
+        trace_ms += st["trace_ms"]
+        trace_launches += st["trace_launches"]
+        rays_local += st["primary_rays"] + st["extension_rays"] + st["shadow_rays"]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+
+    t = torch.tensor([elapsed, float(rays_local), trace_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        t_max = t.clone()
+        dist.all_reduce(t_max[0:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+        elapsed = float(t_max[0].item())
+        rays_total = float(t[1].item())
+    else:
+        rays_total = float(rays_local)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    mrays = rays_total / elapsed / 1e6
+    rays_frame_local = st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"]
+    # roofline: traversal kernels (k_extend + k_shadow), algorithmic bytes per
+    # 32 B ray + 16 B hit + 64 B/node visit + 48 B/prim test
+    per_launch_bytes = st_bytes["trace_bytes"] / max(1, st_bytes["trace_launches"])
+    per_launch_ms = trace_ms / max(1, trace_launches)
+    achieved_gbs = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu = cpu_baseline(desc, args)
+
+    if rank == 0:
+        if args.save:
+            from tools import imgio
+
+            img = (full if world > 1 else pt.buffers.get(FINAL_RESULT)).cpu().numpy()
+            imgio.save_render(args.save, img.reshape(args.height, args.width, 4))
+        out = {
+            "metric": "Mrays/sec + ms/frame, 1M-tri scene @1920x1080 8spp; 1/2/4/8-GPU scaling",
+            "value": round(mrays, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural sphere field, PCG64 seed 1)",
+            "config": {"workload": f"config4: {n_prims:,}-primitive sphere field ({tris:,} tris), "
+                                   f"{args.width}x{args.height}, {args.spp} spp, max_depth {args.max_depth}",
+                       "frame": f"{args.spp} x PTPass::OnRun", "parallelism": f"tiles{args.tile}x{world}",
+                       "rays_per_frame": rays_total / args.steps,
+                       "path_samples_per_s": round(args.width * args.height * args.spp / (ms_per_step * 1e-3), 1),
+                       "bvh_build_ms": round(st_bytes["build_ms"], 3),
+                       "avg_node_visits_per_ray": round(st_bytes["node_visits"] / max(1, rays_frame_local), 2),
+                       "avg_prim_tests_per_ray": round(st_bytes["prim_tests"] / max(1, rays_frame_local), 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "k_extend+k_shadow (BVH traversal)",
+                         "bytes_per_launch": round(per_launch_bytes, 1),
+                         "ms_per_launch": round(per_launch_ms, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(desc, args):
+    """The CPU oracle (scalar C++ restatement, own SAH BVH) on a bounded sample
+    of the same frame: every k-th pixel, all spp, timed with steady_clock."""
+    try:
+        import oracle
+    except Exception as e:  # pragma: no cover
+        return {"error": str(e)}
+    import platform
+
+    osc = oracle.OracleScene(desc)
+    npix = args.width * args.height
+    pixels = np.arange(0, npix, args.cpu_sample_stride, dtype=np.uint32)
+    r = osc.render(spp=args.spp, max_depth=args.max_depth, pixels=pixels, threads=args.cpu_threads)
+    s = r["stats"]
+    rays = s["primary_rays"] + s["extension_rays"] + s["shadow_rays"]
+    cpu_model = platform.processor()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    osc.close()
+    return {"value": round(rays / s["seconds"] / 1e6, 3), "unit": "Mrays/s", "cores": int(s["threads"]),
+            "kind": "port",
+            "sample": f"every {args.cpu_sample_stride}th pixel ({len(pixels)} px) x {args.spp} spp of the same frame, "
+                      f"{rays} rays in {s['seconds']:.2f}s",
+            "cpu": cpu_model}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,268 @@
+/*
+ * pupil_pt.h — C ABI of the MI355X wavefront path tracer (libpupil_pt.so).
+ *
+ * This is the drop-in boundary for the reference's OptiX path-tracing pass
+ * (example/path_tracer).  Every entry point below replaces one piece of the
+ * reference's launch surface:
+ *
+ *   pupil_pt_create          — optix::Pass::InitPipeline + PTPass::SetScene + World::GetIASHandle
+ *                              (example/path_tracer/pt_pass.cpp:29-37,107-209;
+ *                               framework/world/gas_manager.cpp:61-185, ias_manager.cpp:29-114)
+ *   pupil_pt_set_camera      — CameraHelper::GetCudaMemory upload (framework/world/camera.cpp:72-91)
+ *   pupil_pt_update_instance — IASManager::UpdateInstance + IAS::Update refit
+ *                              (framework/world/ias_manager.cpp:116-151,187-211)
+ *   pupil_pt_render          — PTPass::OnRun: optixLaunch(w,h,1) + sync, repeated spp times
+ *                              with random_seed++ / sample_cnt += accumulate
+ *                              (example/path_tracer/pt_pass.cpp:39-57, main.cu:36-194)
+ *   pupil_pt_stats           — no reference equivalent (ray / traversal counters)
+ *   pupil_pt_destroy         — pass + world GPU resource teardown
+ *
+ * The scene crosses the boundary as plain arrays (pupil_scene_desc).  The C++
+ * host layer (Pupil::world::World, Pupil::resource::Scene, see
+ * pupiloptixlab_amd/csrc/host) produces it from mitsuba-style XML exactly as
+ * the reference's World::LoadScene does (framework/world/world.cpp:101-139).
+ *
+ * Error convention (the reference logs then asserts, framework/cuda/util.h:15-26):
+ * every function returns PUPIL_OK (0) or a negative PUPIL_ERR_* code; no C++
+ * exception crosses this boundary; pupil_last_error() returns the message of
+ * the last failure on the calling thread.
+ *
+ * Threading: an engine may be driven from any thread (the device is set on
+ * every call); calls on one engine must not overlap (the reference serialises
+ * SetScene and OnRun under System::m_render_system_mutex, system.cpp:93-173).
+ */
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PUPIL_OK 0
+#define PUPIL_ERR_INVALID -1
+#define PUPIL_ERR_HIP -2
+#define PUPIL_ERR_OOM -3
+#define PUPIL_ERR_IO -4
+#define PUPIL_ERR_UNSUPPORTED -5
+
+/* util::ETextureType (framework/util/texture.h:22-26) */
+#define PUPIL_TEX_RGB 0u
+#define PUPIL_TEX_BITMAP 1u
+#define PUPIL_TEX_CHECKERBOARD 2u
+
+/* EMatType order = framework/decl/material_decl.inl:3-11 (Unknown = 0) */
+#define PUPIL_MAT_UNKNOWN 0u
+#define PUPIL_MAT_DIFFUSE 1u
+#define PUPIL_MAT_DIELECTRIC 2u
+#define PUPIL_MAT_ROUGH_DIELECTRIC 3u
+#define PUPIL_MAT_CONDUCTOR 4u
+#define PUPIL_MAT_ROUGH_CONDUCTOR 5u
+#define PUPIL_MAT_PLASTIC 6u
+#define PUPIL_MAT_ROUGH_PLASTIC 7u
+#define PUPIL_MAT_COUNT 8u
+
+/* optix::EEmitterType (framework/render/emitter/types.h:7-14) */
+#define PUPIL_EMITTER_NONE 0u
+#define PUPIL_EMITTER_TRI_AREA 1u
+#define PUPIL_EMITTER_SPHERE 2u
+#define PUPIL_EMITTER_CONST_ENV 3u
+#define PUPIL_EMITTER_ENV_MAP 4u
+
+#define PUPIL_SHAPE_MESH 0u
+#define PUPIL_SHAPE_SPHERE 1u
+
+/* cuda::Texture (framework/cuda/texture.h:10-57): rgb colour, checkerboard
+ * patches, or an RGBA float bitmap; `transform` is the row-major 4x4 to_uv
+ * matrix whose rows 0 and 1 map (u, v, 0, 1). */
+typedef struct pupil_texture {
+    uint32_t type;
+    float c0[3];          /* RGB colour, or checkerboard patch1 */
+    float c1[3];          /* checkerboard patch2 */
+    float transform[16];  /* row-major */
+    uint32_t width, height;
+    uint32_t filter;      /* BITMAP: 0 point, 1 bilinear (util::ETextureFilterMode) */
+    uint32_t pad;
+    const float *rgba;    /* host pointer, width*height*4 floats (BITMAP only) */
+} pupil_texture;
+
+/* resource::Material (framework/resource/material.h:60-77) flattened.
+ * Texture slot meaning per type (same order as the reference's loaders,
+ * framework/resource/material.cpp:26-147):
+ *   diffuse:          tex[0]=reflectance
+ *   dielectric:       tex[0]=specular_reflectance tex[1]=specular_transmittance
+ *   rough_dielectric: tex[0]=alpha tex[1]=specular_reflectance tex[2]=specular_transmittance
+ *   conductor:        tex[0]=eta tex[1]=k tex[2]=specular_reflectance
+ *   rough_conductor:  tex[0]=alpha tex[1]=eta tex[2]=k tex[3]=specular_reflectance
+ *   plastic:          tex[0]=diffuse_reflectance tex[1]=specular_reflectance
+ *   rough_plastic:    tex[0]=alpha tex[1]=diffuse_reflectance tex[2]=specular_reflectance */
+typedef struct pupil_material {
+    uint32_t type;
+    uint32_t twosided;
+    float int_ior, ext_ior;
+    uint32_t nonlinear;
+    pupil_texture tex[4];
+} pupil_material;
+
+/* resource::Shape (framework/resource/shape.h:34-60): object-space mesh or the
+ * unit sphere (centre 0, radius 1; radius/centre live in the instance transform,
+ * shape.cpp:106-125,196-197). */
+typedef struct pupil_shape {
+    uint32_t kind;
+    uint32_t num_vertices, num_faces;
+    const float *positions;  /* 3 * num_vertices */
+    const float *normals;    /* 3 * num_vertices or NULL */
+    const float *texcoords;  /* 2 * num_vertices or NULL */
+    const uint32_t *indices; /* 3 * num_faces */
+} pupil_shape;
+
+/* world::RenderObject + pt::HitGroupData (render_object.cpp:10-38, type.h:35-39).
+ * to_world/to_object are the row-major 3x4 instance matrix and its inverse
+ * (OptixInstance::transform = Transform.matrix.e[0..11], ias_manager.cpp:171). */
+typedef struct pupil_instance {
+    uint32_t shape;
+    uint32_t material;
+    float to_world[12];
+    float to_object[12];
+    uint32_t flip_normals;
+    uint32_t flip_tex_coords;
+    int32_t emitter_offset; /* first area-emitter index of this instance, -1 if not emissive */
+    uint32_t pad;
+} pupil_instance;
+
+/* optix::Emitter (framework/render/emitter.h:13-24 + emitter/{area,sphere,env}.h) */
+typedef struct pupil_emitter {
+    uint32_t type;
+    float weight;
+    float select_probability;
+    float area;
+    pupil_texture radiance;
+    float pos[3][3];   /* TriArea: world-space vertices */
+    float nrm[3][3];   /* TriArea: world-space vertex normals */
+    float tex[3][2];   /* TriArea: vertex texcoords */
+    float center[3];   /* Sphere centre / env centre */
+    float radius;      /* Sphere radius */
+    float color[3];    /* ConstEnv colour */
+    /* EnvMap: radiance.type == BITMAP; the CDF tables are built by the engine */
+    float to_world[9]; /* EnvMap: rows of the 3x3 rotation */
+    float to_local[9];
+    float scale;
+} pupil_emitter;
+
+typedef struct pupil_scene_desc {
+    uint32_t width, height;    /* film (scene.cpp:86-95) */
+    uint32_t max_depth;        /* integrator (scene.cpp:79-82) */
+    uint32_t pad0;
+    float sample_to_camera[16]; /* optix::Camera (render/camera.h:7-10), row-major */
+    float camera_to_world[16];
+    uint32_t num_shapes;
+    uint32_t num_materials;
+    uint32_t num_instances;
+    uint32_t num_area_emitters;
+    const pupil_shape *shapes;
+    const pupil_material *materials;
+    const pupil_instance *instances;
+    const pupil_emitter *area_emitters; /* EmitterGroup::areas, select_probability filled */
+    const pupil_emitter *env;           /* EmitterGroup::env or NULL */
+} pupil_scene_desc;
+
+/* Output views: caller-owned device buffers (BufferManager in the reference,
+ * framework/system/buffer.h:44-63).  Any pointer except accum may be NULL.
+ * If `compact` is non-zero, buffers are indexed by the rank-local pixel index
+ * (see pupil_pt_launch.tile_*), otherwise by y*width+x. */
+typedef struct pupil_pt_frame {
+    void *accum;  /* float4 "pt accum buffer" */
+    void *frame;  /* float4 "final result" */
+    void *albedo; /* float3 "albedo" */
+    void *normal; /* float3 "normal" */
+    void *test;   /* float  "test" */
+    uint32_t compact;
+    uint32_t pad;
+} pupil_pt_frame;
+
+/* One call renders `spp` consecutive frames exactly as spp calls of
+ * PTPass::OnRun would (pt_pass.cpp:51-56): frame i uses
+ * random_seed = random_seed + i and sample_cnt = sample_cnt + i*accumulate.
+ * Tile sharding: the image is cut into tile_size x tile_size tiles numbered
+ * row-major; this call renders the tiles t with t % tile_world == tile_rank.
+ * tile_world = 1 renders the whole image. */
+typedef struct pupil_pt_launch {
+    uint32_t random_seed;
+    uint32_t sample_cnt;
+    uint32_t spp;
+    uint32_t max_depth; /* 0 = scene value */
+    uint32_t accumulate;
+    uint32_t tile_size;
+    uint32_t tile_rank;
+    uint32_t tile_world;
+    uint32_t collect_stats; /* count node visits / triangle tests (slower) */
+    uint32_t pad;
+} pupil_pt_launch;
+
+typedef struct pupil_pt_counters {
+    uint64_t primary_rays;
+    uint64_t extension_rays;
+    uint64_t shadow_rays;
+    uint64_t path_samples;
+    uint64_t node_visits;    /* only when collect_stats */
+    uint64_t prim_tests;     /* only when collect_stats */
+    uint64_t bvh_nodes;
+    uint64_t bvh_prims;
+    double build_ms;
+    double last_render_ms;   /* device time of the last pupil_pt_render (events) */
+    double trace_ms;         /* device time of the traversal kernels in the last render */
+    double trace_bytes;      /* algorithmic bytes of the traversal kernels (collect_stats) */
+    uint64_t trace_launches;
+} pupil_pt_counters;
+
+typedef struct pupil_pt pupil_pt;
+
+const char *pupil_last_error(void);
+int pupil_abi_version(void);
+
+int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out);
+int pupil_pt_set_camera(pupil_pt *pt, const float sample_to_camera[16], const float camera_to_world[16]);
+int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_world[12], const float to_object[12]);
+int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_launch *launch, void *hip_stream);
+int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out);
+int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank,
+                          uint32_t tile_world, uint32_t *out_pixels, uint32_t *inout_count);
+void pupil_pt_destroy(pupil_pt *pt);
+
+/* ---- verification entry points (used by the parity tests) ----
+ * closest (any_hit = 0) or any hit (any_hit = 1) for n host rays packed as
+ * (ox, oy, oz, dx, dy, dz, tmin, tmax); out (host) = (t, b1, b2, prim id bits)
+ * per ray, prim id = 0xFFFFFFFF and t = -1 on a miss (any hit: t = 1 if occluded). */
+int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out, int any_hit);
+/* evaluates the device's sin, cos, acos, atan2(x, y2), sqrt, 1/x on n inputs:
+ * out[6*i + k] for k in that order (bit-exactness probe for the CPU oracle) */
+int pupil_debug_math(int device, uint32_t n, const float *x, const float *y2, float *out);
+
+/* ---- host world (the reference's resource::Scene + world::World, C++ inside) ---- */
+typedef struct pupil_world pupil_world;
+
+int pupil_world_create(pupil_world **out);
+/* mitsuba-3 XML subset, resource/scene.cpp:27-227 semantics */
+int pupil_world_load_xml(pupil_world *w, const char *path);
+/* programmatic scene building (procedural benchmark scenes) */
+int pupil_world_set_film(pupil_world *w, uint32_t width, uint32_t height, uint32_t max_depth);
+/* sensor: fov in degrees along fov_axis ('x' or 'y'), to_world row-major 4x4 in mitsuba convention */
+int pupil_world_set_sensor(pupil_world *w, float fov, char fov_axis, float near_clip, float far_clip,
+                           const float to_world[16]);
+int pupil_world_add_mesh(pupil_world *w, uint32_t num_vertices, uint32_t num_faces, const float *positions,
+                         const float *normals, const float *texcoords, const uint32_t *indices, uint32_t *out_shape);
+int pupil_world_add_builtin_shape(pupil_world *w, const char *name /* rectangle|cube|sphere */, uint32_t *out_shape);
+int pupil_world_add_material(pupil_world *w, const pupil_material *m, uint32_t *out_material);
+/* is_emitter: area emitter with the given radiance texture */
+int pupil_world_add_instance(pupil_world *w, uint32_t shape, uint32_t material, const float to_world[16],
+                             uint32_t flip_normals, uint32_t flip_tex_coords, uint32_t is_emitter,
+                             const pupil_texture *radiance, uint32_t *out_instance);
+int pupil_world_add_const_env(pupil_world *w, const float radiance[3]);
+/* resolves emitters (EmitterHelper), camera matrices (CameraHelper) and fills desc;
+ * pointers stay valid until the world is modified or destroyed */
+int pupil_world_get_desc(pupil_world *w, pupil_scene_desc *desc);
+void pupil_world_destroy(pupil_world *w);
+
+#ifdef __cplusplus
+}
+#endif

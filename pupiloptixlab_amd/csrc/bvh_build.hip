@@ -1,0 +1,441 @@
+// bvh_build.hip — GPU LBVH builder (replaces optixAccelBuild for the GAS/IAS,
+// framework/world/gas_manager.cpp:130-173, ias_manager.cpp:54-96).
+//
+// Pipeline (all on device, one stream):
+//   1. k_prim_setup    object-space meshes -> world-space primitive records +
+//                      AABBs (instances flattened; spheres keep their instance)
+//   2. k_bounds        scene centroid bounds (wave reduce + ordered-int atomics)
+//   3. k_morton        30-bit Morton code of each centroid
+//   4. radix sort      hand-written stable LSD sort, 8-bit digits, wave-ballot
+//                      multisplit ranking (k_sort_hist / k_sort_scan / k_sort_scatter)
+//   5. k_karras        Karras 2012 hierarchy over the sorted codes (index-augmented)
+//   6. k_refit         bottom-up AABBs, agent-scope release/acquire per arrival
+//   7. k_emit          64 B BVH2 nodes; subtrees of <= leaf_size primitives
+//                      collapse into one leaf (their primitives are contiguous)
+//   8. k_reorder       primitive records in Morton order (leaf ranges index them)
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "pt_kernels.h"
+
+namespace pupil {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct Aabb {
+    float lo[3];
+    float hi[3];
+};
+
+__device__ __forceinline__ uint32_t float_to_ordered(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ordered_to_float(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+__global__ void k_prim_setup(BvhBuildInput in, float4 *recs, Aabb *boxes) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.num_prims) return;
+    const uint32_t inst_id = in.prim_inst[i];
+    const DevInstance &inst = in.instances[inst_id];
+    const uint32_t mtype = in.materials[inst.material].type;
+    const uint32_t bin = (mtype >= 1u && mtype <= 7u) ? mtype : 8u;
+    Aabb b;
+    if (inst.kind == PUPIL_SHAPE_SPHERE) {
+        const float *m = inst.to_world;
+        const vec3 c = v3(m[3], m[7], m[11]);
+        // exact extents of an affinely transformed unit sphere, padded
+        const float ex = sqrtf(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.0001f;
+        const float ey = sqrtf(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.0001f;
+        const float ez = sqrtf(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.0001f;
+        b.lo[0] = c.x - ex; b.lo[1] = c.y - ey; b.lo[2] = c.z - ez;
+        b.hi[0] = c.x + ex; b.hi[1] = c.y + ey; b.hi[2] = c.z + ez;
+        recs[3 * i + 0] = make_float4(c.x, c.y, c.z, __uint_as_float(i | kPrimSphereBit));
+        recs[3 * i + 1] = make_float4(ex, ey, ez, __uint_as_float(inst_id));
+        recs[3 * i + 2] = make_float4(0.f, 0.f, 0.f, __uint_as_float(bin));
+    } else {
+        const uint32_t local = i - inst.prim_offset;
+        const uint32_t i0 = inst.indices[3 * local], i1 = inst.indices[3 * local + 1], i2 = inst.indices[3 * local + 2];
+        const float *P = inst.positions;
+        // world-space vertices: the CPU oracle applies the same row-major 3x4 product
+        const vec3 w0 = xform_point(inst.to_world, v3(P[3 * i0], P[3 * i0 + 1], P[3 * i0 + 2]));
+        const vec3 w1 = xform_point(inst.to_world, v3(P[3 * i1], P[3 * i1 + 1], P[3 * i1 + 2]));
+        const vec3 w2 = xform_point(inst.to_world, v3(P[3 * i2], P[3 * i2 + 1], P[3 * i2 + 2]));
+        b.lo[0] = fminf(fminf(w0.x, w1.x), w2.x);
+        b.lo[1] = fminf(fminf(w0.y, w1.y), w2.y);
+        b.lo[2] = fminf(fminf(w0.z, w1.z), w2.z);
+        b.hi[0] = fmaxf(fmaxf(w0.x, w1.x), w2.x);
+        b.hi[1] = fmaxf(fmaxf(w0.y, w1.y), w2.y);
+        b.hi[2] = fmaxf(fmaxf(w0.z, w1.z), w2.z);
+        recs[3 * i + 0] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(i));
+        recs[3 * i + 1] = make_float4(w1.x, w1.y, w1.z, __uint_as_float(inst_id));
+        recs[3 * i + 2] = make_float4(w2.x, w2.y, w2.z, __uint_as_float(bin));
+    }
+    boxes[i] = b;
+}
+
+// centroid bounds -> 6 ordered uints (lo xyz as min, hi xyz as max)
+__global__ void k_bounds(const Aabb *boxes, uint32_t n, uint32_t *out) {
+    float lo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+    float hi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const Aabb b = boxes[i];
+        for (int k = 0; k < 3; k++) {
+            const float c = 0.5f * (b.lo[k] + b.hi[k]);
+            lo[k] = fminf(lo[k], c);
+            hi[k] = fmaxf(hi[k], c);
+        }
+    }
+    for (int k = 0; k < 3; k++) {
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        for (int k = 0; k < 3; k++) {
+            atomicMin(&out[k], float_to_ordered(lo[k]));
+            atomicMax(&out[3 + k], float_to_ordered(hi[k]));
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t expand_bits(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+__global__ void k_morton(const Aabb *boxes, uint32_t n, const uint32_t *bounds, uint32_t *keys, uint32_t *vals) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float lo[3], ext[3];
+    for (int k = 0; k < 3; k++) {
+        lo[k] = ordered_to_float(bounds[k]);
+        const float h = ordered_to_float(bounds[3 + k]);
+        ext[k] = h - lo[k];
+    }
+    const Aabb b = boxes[i];
+    uint32_t q[3];
+    for (int k = 0; k < 3; k++) {
+        const float c = 0.5f * (b.lo[k] + b.hi[k]);
+        float t = ext[k] > 0.f ? (c - lo[k]) / ext[k] : 0.5f;
+        t = fminf(fmaxf(t * 1024.f, 0.f), 1023.f);
+        q[k] = (uint32_t)t;
+    }
+    keys[i] = (expand_bits(q[0]) << 2) | (expand_bits(q[1]) << 1) | expand_bits(q[2]);
+    vals[i] = i;
+}
+
+// ---------------------------------------------------------------- radix sort
+constexpr int kSortItems = 16;
+constexpr int kSortTile = kBlock * kSortItems;
+
+__global__ __launch_bounds__(kBlock) void k_sort_hist(const uint32_t *keys, uint32_t n, int shift, uint32_t *hist,
+                                                      uint32_t nblocks) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * kSortTile;
+    for (int j = 0; j < kSortItems; j++) {
+        const uint32_t i = base + j * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];  // digit-major
+}
+
+// single-block exclusive scan of `count` entries (in place)
+__global__ __launch_bounds__(1024) void k_sort_scan(uint32_t *data, uint32_t count) {
+    __shared__ uint32_t partial[1024];
+    const uint32_t per = (count + 1023) / 1024;
+    const uint32_t begin = threadIdx.x * per;
+    const uint32_t end = min(begin + per, count);
+    uint32_t sum = 0;
+    for (uint32_t i = begin; i < end; i++) sum += data[i];
+    partial[threadIdx.x] = sum;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over 1024 partial sums
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = threadIdx.x >= off ? partial[threadIdx.x - off] : 0u;
+        __syncthreads();
+        partial[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = threadIdx.x > 0 ? partial[threadIdx.x - 1] : 0u;
+    for (uint32_t i = begin; i < end; i++) {
+        const uint32_t v = data[i];
+        data[i] = run;
+        run += v;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const uint32_t *keys_in, const uint32_t *vals_in,
+                                                         uint32_t *keys_out, uint32_t *vals_out, uint32_t n, int shift,
+                                                         const uint32_t *offsets, uint32_t nblocks) {
+    constexpr int kWaves = kBlock / 64;
+    __shared__ uint32_t wave_count[kWaves][256];
+    __shared__ uint32_t wave_off[kWaves][256];
+    __shared__ uint32_t running[256];
+    running[threadIdx.x] = offsets[threadIdx.x * nblocks + blockIdx.x];
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const uint32_t base = blockIdx.x * kSortTile;
+    for (int j = 0; j < kSortItems; j++) {
+        for (int w = 0; w < kWaves; w++) wave_count[w][threadIdx.x] = 0;
+        __syncthreads();
+        const uint32_t i = base + j * kBlock + threadIdx.x;
+        const bool valid = i < n;
+        uint32_t key = 0, val = 0, digit = 0;
+        if (valid) {
+            key = keys_in[i];
+            val = vals_in[i];
+            digit = (key >> shift) & 0xFFu;
+        }
+        unsigned long long peers = __ballot(valid);
+        for (int b = 0; b < 8; b++) {
+            const bool bit = (digit >> b) & 1u;
+            const unsigned long long bal = __ballot(bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        if (valid && rank == 0) wave_count[wave][digit] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        {
+            const uint32_t d = threadIdx.x;
+            uint32_t r = running[d];
+            for (int w = 0; w < kWaves; w++) {
+                wave_off[w][d] = r;
+                r += wave_count[w][d];
+            }
+            running[d] = r;
+        }
+        __syncthreads();
+        if (valid) {
+            const uint32_t pos = wave_off[wave][digit] + rank;
+            keys_out[pos] = key;
+            vals_out[pos] = val;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- Karras 2012
+__device__ __forceinline__ int delta(const uint32_t *keys, int n, int i, int j) {
+    if (j < 0 || j >= n) return -1;
+    const uint32_t a = keys[i], b = keys[j];
+    if (a == b) return 32 + __clz((uint32_t)i ^ (uint32_t)j);
+    return __clz(a ^ b);
+}
+
+__global__ void k_karras(const uint32_t *keys, int n, int2 *children, int2 *ranges, int *parent_internal,
+                         int *parent_leaf) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1) return;
+    const int d = (delta(keys, n, i, i + 1) - delta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
+    const int dmin = delta(keys, n, i, i - d);
+    int lmax = 2;
+    while (delta(keys, n, i, i + lmax * d) > dmin) lmax <<= 1;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (delta(keys, n, i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = delta(keys, n, i, j);
+    int s = 0;
+    int t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (delta(keys, n, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    const int gamma = i + s * d + min(d, 0);
+    const int first = min(i, j), last = max(i, j);
+    // child encoding here: >= 0 internal, < 0 -> leaf ~prim
+    const int left = (first == gamma) ? ~gamma : gamma;
+    const int right = (last == gamma + 1) ? ~(gamma + 1) : gamma + 1;
+    children[i] = make_int2(left, right);
+    ranges[i] = make_int2(first, last);
+    if (left >= 0) parent_internal[left] = i;
+    else parent_leaf[gamma] = i;
+    if (right >= 0) parent_internal[right] = i;
+    else parent_leaf[gamma + 1] = i;
+}
+
+__device__ __forceinline__ Aabb merge(const Aabb &a, const Aabb &b) {
+    Aabb r;
+    for (int k = 0; k < 3; k++) {
+        r.lo[k] = fminf(a.lo[k], b.lo[k]);
+        r.hi[k] = fmaxf(a.hi[k], b.hi[k]);
+    }
+    return r;
+}
+
+// Bottom-up refit.  The second thread to arrive at a node merges both
+// children.  Bounds are published with an agent-scope release before the
+// arrival atomic and read after an agent-scope acquire (L1s are per CU and the
+// per-XCD L2s are not coherent, MI355X_MICROARCH.md "inter-workgroup visibility").
+__global__ void k_refit(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
+                        const int *parent_internal, const int *parent_leaf, Aabb *node_boxes, uint32_t *flags) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int node = parent_leaf[i];
+    while (node >= 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const uint32_t prev = __hip_atomic_fetch_add(&flags[node], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == 0u) return;  // first arrival: the sibling finishes the node
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const int2 c = children[node];
+        const Aabb a = c.x >= 0 ? node_boxes[c.x] : prim_boxes[sorted_vals[~c.x]];
+        const Aabb b = c.y >= 0 ? node_boxes[c.y] : prim_boxes[sorted_vals[~c.y]];
+        node_boxes[node] = merge(a, b);
+        node = node == 0 ? -1 : parent_internal[node];
+    }
+}
+
+__device__ __forceinline__ int child_link(int c, const int2 *ranges, uint32_t leaf_size) {
+    if (c < 0) return make_leaf((uint32_t)~c, 1u);
+    const int2 r = ranges[c];
+    const uint32_t cnt = (uint32_t)(r.y - r.x + 1);
+    if (cnt <= leaf_size) return make_leaf((uint32_t)r.x, cnt);
+    return c;
+}
+
+__global__ void k_emit(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
+                       const int2 *ranges, const Aabb *node_boxes, uint32_t leaf_size, BvhNode *nodes) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1) return;
+    const int2 c = children[i];
+    const Aabb a = c.x >= 0 ? node_boxes[c.x] : prim_boxes[sorted_vals[~c.x]];
+    const Aabb b = c.y >= 0 ? node_boxes[c.y] : prim_boxes[sorted_vals[~c.y]];
+    BvhNode nd;
+    nd.lo0 = make_float4(a.lo[0], a.lo[1], a.lo[2], __int_as_float(child_link(c.x, ranges, leaf_size)));
+    nd.hi0 = make_float4(a.hi[0], a.hi[1], a.hi[2], __int_as_float(child_link(c.y, ranges, leaf_size)));
+    nd.lo1 = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f);
+    nd.hi1 = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
+    nodes[i] = nd;
+}
+
+__global__ void k_reorder(int n, const uint32_t *sorted_vals, const float4 *recs_in, float4 *recs_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t src = sorted_vals[i];
+    recs_out[3 * i + 0] = recs_in[3 * src + 0];
+    recs_out[3 * i + 1] = recs_in[3 * src + 1];
+    recs_out[3 * i + 2] = recs_in[3 * src + 2];
+}
+
+template <typename T>
+hipError_t dmalloc(T **p, size_t count) {
+    return hipMalloc((void **)p, sizeof(T) * (count > 0 ? count : 1));
+}
+
+}  // namespace
+
+void free_lbvh(BvhBuildOutput &out) {
+    if (out.nodes) (void)hipFree(out.nodes);
+    if (out.prims) (void)hipFree(out.prims);
+    out.nodes = nullptr;
+    out.prims = nullptr;
+}
+
+int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms) {
+    const int n = (int)in.num_prims;
+    if (n <= 0) return -1;
+    if (leaf_size < 1) leaf_size = 1;
+    if (leaf_size > (uint32_t)kLeafMax) leaf_size = kLeafMax;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, s);
+
+    float4 *recs = nullptr;
+    Aabb *boxes = nullptr, *node_boxes = nullptr;
+    uint32_t *bounds = nullptr, *keys = nullptr, *vals = nullptr, *keys2 = nullptr, *vals2 = nullptr, *hist = nullptr,
+             *flags = nullptr;
+    int2 *children = nullptr, *ranges = nullptr;
+    int *parent_internal = nullptr, *parent_leaf = nullptr;
+    const uint32_t nblocks = (uint32_t)((n + kSortTile - 1) / kSortTile);
+    hipError_t err = hipSuccess;
+    err = dmalloc(&recs, 3 * (size_t)n);
+    if (!err) err = dmalloc(&boxes, n);
+    if (!err) err = dmalloc(&node_boxes, n);
+    if (!err) err = dmalloc(&bounds, 6);
+    if (!err) err = dmalloc(&keys, n);
+    if (!err) err = dmalloc(&vals, n);
+    if (!err) err = dmalloc(&keys2, n);
+    if (!err) err = dmalloc(&vals2, n);
+    if (!err) err = dmalloc(&hist, 256 * (size_t)nblocks);
+    if (!err) err = dmalloc(&flags, n);
+    if (!err) err = dmalloc(&children, n);
+    if (!err) err = dmalloc(&ranges, n);
+    if (!err) err = dmalloc(&parent_internal, n);
+    if (!err) err = dmalloc(&parent_leaf, n);
+    if (!err) err = dmalloc(&out.nodes, n > 1 ? (size_t)(n - 1) : 1);
+    if (!err) err = dmalloc(&out.prims, 3 * (size_t)n);
+    if (err) {
+        free_lbvh(out);
+    } else {
+        const uint32_t g = (uint32_t)((n + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(k_prim_setup, dim3(g), dim3(kBlock), 0, s, in, recs, boxes);
+        const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+        (void)hipMemcpyAsync(bounds, init, sizeof(init), hipMemcpyHostToDevice, s);
+        hipLaunchKernelGGL(k_bounds, dim3(min(g, 1024u)), dim3(kBlock), 0, s, boxes, (uint32_t)n, bounds);
+        hipLaunchKernelGGL(k_morton, dim3(g), dim3(kBlock), 0, s, boxes, (uint32_t)n, bounds, keys, vals);
+        uint32_t *ki = keys, *vi = vals, *ko = keys2, *vo = vals2;
+        for (int shift = 0; shift < 30; shift += 8) {
+            hipLaunchKernelGGL(k_sort_hist, dim3(nblocks), dim3(kBlock), 0, s, ki, (uint32_t)n, shift, hist, nblocks);
+            hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist, 256u * nblocks);
+            hipLaunchKernelGGL(k_sort_scatter, dim3(nblocks), dim3(kBlock), 0, s, ki, vi, ko, vo, (uint32_t)n, shift,
+                               hist, nblocks);
+            uint32_t *t = ki; ki = ko; ko = t;
+            t = vi; vi = vo; vo = t;
+        }
+        // ki/vi hold the sorted keys/values
+        if (n > 1) {
+            (void)hipMemsetAsync(parent_internal, 0xFF, sizeof(int) * n, s);
+            (void)hipMemsetAsync(flags, 0, sizeof(uint32_t) * n, s);
+            const uint32_t gi = (uint32_t)((n - 1 + kBlock - 1) / kBlock);
+            hipLaunchKernelGGL(k_karras, dim3(gi), dim3(kBlock), 0, s, ki, n, children, ranges, parent_internal,
+                               parent_leaf);
+            hipLaunchKernelGGL(k_refit, dim3(g), dim3(kBlock), 0, s, n, vi, boxes, children, parent_internal,
+                               parent_leaf, node_boxes, flags);
+            hipLaunchKernelGGL(k_emit, dim3(gi), dim3(kBlock), 0, s, n, vi, boxes, children, ranges, node_boxes,
+                               leaf_size, out.nodes);
+        }
+        hipLaunchKernelGGL(k_reorder, dim3(g), dim3(kBlock), 0, s, n, vi, recs, out.prims);
+        out.num_nodes = n > 1 ? (uint32_t)(n - 1) : 0u;
+        out.root_link = ((uint32_t)n <= leaf_size) ? (uint32_t)make_leaf(0u, (uint32_t)n) : 0u;
+        err = hipGetLastError();
+    }
+    (void)hipEventRecord(e1, s);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (build_ms) *build_ms = ms;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    hipFree(recs);
+    hipFree(boxes);
+    hipFree(node_boxes);
+    hipFree(bounds);
+    hipFree(keys);
+    hipFree(vals);
+    hipFree(keys2);
+    hipFree(vals2);
+    hipFree(hist);
+    hipFree(flags);
+    hipFree(children);
+    hipFree(ranges);
+    hipFree(parent_internal);
+    hipFree(parent_leaf);
+    return err == hipSuccess ? 0 : -2;
+}
+
+}  // namespace pupil

@@ -1,0 +1,654 @@
+// engine.hip — host side of the HIP path tracer and the C ABI (include/pupil_pt.h).
+//
+// pupil_pt_create  = PTPass::SetScene + World::GetIASHandle + SBT build
+//                    (example/path_tracer/pt_pass.cpp:107-209): scene arrays are
+//                    copied to engine-owned HBM, materials get the host
+//                    precompute of optix_material.cpp:87-119, the LBVH replaces
+//                    the GAS/IAS.
+// pupil_pt_render  = spp x PTPass::OnRun (pt_pass.cpp:39-57) as one wavefront batch.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pupil_pt.h"
+#include "pt_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                     \
+    do {                                                                                                  \
+        hipError_t _e = (expr);                                                                           \
+        if (_e != hipSuccess)                                                                             \
+            return fail(_e == hipErrorOutOfMemory ? PUPIL_ERR_OOM : PUPIL_ERR_HIP,                        \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                               \
+    } while (0)
+
+using namespace pupil;
+
+// fresnel::DiffuseReflectance (render/material/fresnel.h:67-94)
+float diffuse_reflectance(float eta) {
+    if (eta < 1) {
+        return -1.4399f * (eta * eta) + 0.7099f * eta + 0.6681f + 0.0636f / eta;
+    }
+    const float inv_eta = 1.0f / eta;
+    const float inv_eta2 = inv_eta * inv_eta;
+    const float inv_eta3 = inv_eta2 * inv_eta;
+    const float inv_eta4 = inv_eta3 * inv_eta;
+    const float inv_eta5 = inv_eta4 * inv_eta;
+    return 0.919317f - 3.4793f * inv_eta + 6.75335f * inv_eta2 - 7.80989f * inv_eta3 + 4.98554f * inv_eta4 -
+           1.36881f * inv_eta5;
+}
+
+// GetPixelAverage (optix_material.cpp:15-42)
+vec3 pixel_average(const pupil_texture &t) {
+    if (t.type == PUPIL_TEX_RGB) return v3(t.c0[0], t.c0[1], t.c0[2]);
+    if (t.type == PUPIL_TEX_CHECKERBOARD) {
+        const float r = t.c0[0] + t.c1[0];
+        const float g = t.c0[1] + t.c1[1];
+        const float b = t.c0[2] + t.c1[2];
+        return v3(r, g, b) * 0.5f;
+    }
+    if (t.type == PUPIL_TEX_BITMAP && t.rgba && t.width && t.height) {
+        float r = 0.f, g = 0.f, b = 0.f;
+        for (size_t i = 0, idx = 0; i < t.height; ++i)
+            for (size_t j = 0; j < t.width; ++j) {
+                r += t.rgba[idx++];
+                g += t.rgba[idx++];
+                b += t.rgba[idx++];
+                idx++;
+            }
+        return v3(r, g, b) / (1.f * (float)t.height * (float)t.width);
+    }
+    return v3(0.f);
+}
+
+}  // namespace
+
+namespace Pupil {
+void set_last_error(const std::string &m) { g_last_error = m; }
+}  // namespace Pupil
+
+struct pupil_pt {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    DeviceScene sc{};
+    std::vector<void *> allocs;
+    BvhBuildOutput bvh{};
+    uint32_t width = 0, height = 0, max_depth = 1;
+    uint32_t num_prims = 0;
+    double build_ms = 0.0;
+    // path state / queues (grown on demand)
+    size_t cap = 0;
+    PathState ps{};
+    Queues q{};
+    int *ovf = nullptr;
+    uint32_t ovf_threads = 0;
+    // pixel map cache
+    uint32_t *pixel_map = nullptr;
+    uint32_t pm_key[5] = {0, 0, 0, 0, 0};
+    uint32_t pm_count = 0;
+    // stats
+    unsigned long long *trace_counters = nullptr;  // [0] nodes [1] prims
+    uint32_t *ray_log = nullptr;                   // per bounce: next, shadow
+    uint32_t last_paths = 0, last_bounces = 0;
+    bool last_stats = false;
+    std::vector<hipEvent_t> trace_events;  // pairs
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    uint32_t trace_pairs = 0;
+    pupil_pt_counters totals{};
+
+    template <typename T>
+    hipError_t alloc(T **p, size_t count) {
+        hipError_t e = hipMalloc((void **)p, sizeof(T) * (count ? count : 1));
+        if (e == hipSuccess) allocs.push_back(*p);
+        return e;
+    }
+    template <typename T>
+    hipError_t upload(T **p, const T *src, size_t count) {
+        hipError_t e = alloc(p, count);
+        if (e == hipSuccess && count) e = hipMemcpy(*p, src, sizeof(T) * count, hipMemcpyHostToDevice);
+        return e;
+    }
+    void release_state() {
+        void *bufs[] = {ps.ray_o, ps.ray_d, ps.hit, ps.thr, ps.rad, ps.misc, ps.sh_o, ps.sh_d, ps.sh_c, q.bins, q.next,
+                        q.shadow};
+        for (void *b : bufs)
+            if (b) (void)hipFree(b);
+        ps = PathState{};
+        q.bins = q.next = q.shadow = nullptr;
+        cap = 0;
+    }
+    ~pupil_pt() {
+        (void)hipSetDevice(device);
+        release_state();
+        for (void *p : allocs) (void)hipFree(p);
+        free_lbvh(bvh);
+        if (pixel_map) (void)hipFree(pixel_map);
+        for (auto e : trace_events) (void)hipEventDestroy(e);
+        if (ev_begin) (void)hipEventDestroy(ev_begin);
+        if (ev_end) (void)hipEventDestroy(ev_end);
+        if (own_stream) (void)hipStreamDestroy(own_stream);
+    }
+};
+
+namespace {
+
+int upload_texture(pupil_pt *pt, const pupil_texture &t, DevTexture &d) {
+    std::memset(&d, 0, sizeof(d));
+    d.type = t.type;
+    d.width = t.width;
+    d.height = t.height;
+    d.filter = t.filter;
+    for (int k = 0; k < 3; k++) {
+        d.c0[k] = t.c0[k];
+        d.c1[k] = t.c1[k];
+    }
+    for (int k = 0; k < 4; k++) {
+        d.r0[k] = t.transform[k];
+        d.r1[k] = t.transform[4 + k];
+    }
+    if (t.type == PUPIL_TEX_BITMAP) {
+        if (!t.rgba || !t.width || !t.height) return fail(PUPIL_ERR_INVALID, "bitmap texture without texels");
+        float4 *texels = nullptr;
+        HIP_TRY(pt->upload(&texels, reinterpret_cast<const float4 *>(t.rgba), (size_t)t.width * t.height));
+        d.data = texels;
+    } else if (t.type > PUPIL_TEX_CHECKERBOARD) {
+        return fail(PUPIL_ERR_INVALID, "unknown texture type");
+    }
+    return PUPIL_OK;
+}
+
+int convert_emitter(pupil_pt *pt, const pupil_emitter &e, DevEmitter &d) {
+    std::memset(&d, 0, sizeof(d));
+    d.type = e.type;
+    d.select_probability = e.select_probability;
+    d.area = e.area;
+    d.radius = e.radius;
+    int rc = upload_texture(pt, e.radiance, d.radiance);
+    if (rc) return rc;
+    for (int k = 0; k < 3; k++) {
+        d.pos[k] = v3(e.pos[k][0], e.pos[k][1], e.pos[k][2]);
+        d.nrm[k] = v3(e.nrm[k][0], e.nrm[k][1], e.nrm[k][2]);
+        d.tex[k] = v2(e.tex[k][0], e.tex[k][1]);
+    }
+    d.center = v3(e.center[0], e.center[1], e.center[2]);
+    d.color = v3(e.color[0], e.color[1], e.color[2]);
+    d.scale = e.scale;
+    for (int k = 0; k < 9; k++) {
+        d.to_world[k] = e.to_world[k];
+        d.to_local[k] = e.to_local[k];
+    }
+    if (e.type == PUPIL_EMITTER_ENV_MAP) {
+        // BuildEnvMapCdfTable (world/emitter.cpp:107-149)
+        const pupil_texture &t = e.radiance;
+        if (t.type != PUPIL_TEX_BITMAP || !t.rgba) return fail(PUPIL_ERR_INVALID, "env map needs a bitmap");
+        const size_t w = t.width, h = t.height;
+        std::vector<float> col_cdf((w + 1) * h), row_cdf(h + 1), row_weight(h);
+        size_t ci = 0, ri = 0;
+        float row_sum = 0.f;
+        row_cdf[ri++] = 0.f;
+        for (size_t y = 0; y < h; ++y) {
+            float col_sum = 0.f;
+            col_cdf[ci++] = 0.f;
+            for (size_t x = 0; x < w; ++x) {
+                const size_t pix = y * w + x;
+                col_sum += luminance(v3(t.rgba[pix * 4 + 0], t.rgba[pix * 4 + 1], t.rgba[pix * 4 + 2]));
+                col_cdf[ci++] = col_sum;
+            }
+            for (size_t x = 1; x < w; ++x) col_cdf[ci - x - 1] /= col_sum;
+            col_cdf[ci - 1] = 1.f;
+            const float weight = std::sin((y + 0.5f) * kPi / h);
+            row_weight[y] = weight;
+            row_sum += col_sum * weight;
+            row_cdf[ri++] = row_sum;
+        }
+        for (size_t y = 1; y < h; ++y) row_cdf[ri - y - 1] /= row_sum;
+        row_cdf[ri - 1] = 1.f;
+        d.normalization = 1.f / (row_sum * (2.f * kPi / w) * (kPi / h));
+        d.map_w = (uint32_t)w;
+        d.map_h = (uint32_t)h;
+        float *a = nullptr, *b = nullptr, *c = nullptr;
+        HIP_TRY(pt->upload(&a, row_cdf.data(), row_cdf.size()));
+        HIP_TRY(pt->upload(&b, col_cdf.data(), col_cdf.size()));
+        HIP_TRY(pt->upload(&c, row_weight.data(), row_weight.size()));
+        d.row_cdf = a;
+        d.col_cdf = b;
+        d.row_weight = c;
+    }
+    return PUPIL_OK;
+}
+
+int ensure_state(pupil_pt *pt, size_t paths) {
+    if (paths <= pt->cap) return PUPIL_OK;
+    pt->release_state();
+    const size_t n = paths;
+    HIP_TRY(hipMalloc((void **)&pt->ps.ray_o, sizeof(float4) * n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.ray_d, sizeof(float4) * n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.hit, sizeof(float4) * n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.thr, sizeof(float4) * n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.rad, sizeof(float4) * n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.misc, sizeof(uint4) * n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.sh_o, sizeof(float4) * n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.sh_d, sizeof(float4) * n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.sh_c, sizeof(float4) * n));
+    HIP_TRY(hipMalloc((void **)&pt->q.bins, sizeof(uint32_t) * n * kNumQueues));
+    HIP_TRY(hipMalloc((void **)&pt->q.next, sizeof(uint32_t) * n));
+    HIP_TRY(hipMalloc((void **)&pt->q.shadow, sizeof(uint32_t) * n));
+    pt->q.capacity = (uint32_t)n;
+    pt->cap = n;
+    return PUPIL_OK;
+}
+
+// Local pixel list of a rank: tiles t with t % world == rank, row-major tile
+// order, row-major pixels inside a tile (clipped at the image border).
+uint32_t local_pixels(uint32_t w, uint32_t h, uint32_t ts, uint32_t rank, uint32_t world, uint32_t *out) {
+    if (world <= 1) {
+        if (out)
+            for (uint32_t i = 0; i < w * h; i++) out[i] = i;
+        return w * h;
+    }
+    const uint32_t tx = (w + ts - 1) / ts, ty = (h + ts - 1) / ts;
+    uint32_t n = 0;
+    for (uint32_t t = rank; t < tx * ty; t += world) {
+        const uint32_t bx = (t % tx) * ts, by = (t / tx) * ts;
+        for (uint32_t y = by; y < by + ts && y < h; y++)
+            for (uint32_t x = bx; x < bx + ts && x < w; x++) {
+                if (out) out[n] = y * w + x;
+                n++;
+            }
+    }
+    return n;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *pupil_last_error(void) { return g_last_error.c_str(); }
+int pupil_abi_version(void) { return 1; }
+
+int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank, uint32_t tile_world,
+                          uint32_t *out_pixels, uint32_t *inout_count) {
+    if (!inout_count || width == 0 || height == 0) return fail(PUPIL_ERR_INVALID, "bad arguments");
+    if (tile_world > 1 && (tile_size == 0 || tile_rank >= tile_world)) return fail(PUPIL_ERR_INVALID, "bad tiling");
+    const uint32_t n = local_pixels(width, height, tile_size, tile_rank, tile_world, nullptr);
+    if (out_pixels) {
+        if (*inout_count < n) return fail(PUPIL_ERR_INVALID, "output too small");
+        local_pixels(width, height, tile_size, tile_rank, tile_world, out_pixels);
+    }
+    *inout_count = n;
+    return PUPIL_OK;
+}
+
+int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
+    if (!scene || !out) return fail(PUPIL_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (scene->width == 0 || scene->height == 0) return fail(PUPIL_ERR_INVALID, "empty film");
+    if (scene->num_instances == 0) return fail(PUPIL_ERR_INVALID, "scene has no instances");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PUPIL_ERR_HIP, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(PUPIL_ERR_INVALID, "bad device index");
+    HIP_TRY(hipSetDevice(device));
+    auto pt = new pupil_pt();
+    pt->device = device;
+    auto cleanup = [&](int rc) {
+        delete pt;
+        return rc;
+    };
+    if (hipStreamCreateWithFlags(&pt->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(PUPIL_ERR_HIP, "stream creation failed"));
+    pt->width = scene->width;
+    pt->height = scene->height;
+    pt->max_depth = scene->max_depth ? scene->max_depth : 1;
+
+    // shapes
+    struct ShapeDev {
+        float *pos = nullptr, *nrm = nullptr, *tex = nullptr;
+        uint32_t *idx = nullptr;
+    };
+    std::vector<ShapeDev> shapes(scene->num_shapes);
+    for (uint32_t s = 0; s < scene->num_shapes; s++) {
+        const pupil_shape &sh = scene->shapes[s];
+        if (sh.kind == PUPIL_SHAPE_MESH) {
+            if (!sh.positions || !sh.indices || sh.num_faces == 0)
+                return cleanup(fail(PUPIL_ERR_INVALID, "mesh without positions/indices"));
+            for (size_t i = 0; i < 3 * (size_t)sh.num_faces; i++)
+                if (sh.indices[i] >= sh.num_vertices) return cleanup(fail(PUPIL_ERR_INVALID, "index out of range"));
+            if (pt->upload(&shapes[s].pos, sh.positions, 3 * (size_t)sh.num_vertices) ||
+                (sh.normals && pt->upload(&shapes[s].nrm, sh.normals, 3 * (size_t)sh.num_vertices)) ||
+                (sh.texcoords && pt->upload(&shapes[s].tex, sh.texcoords, 2 * (size_t)sh.num_vertices)) ||
+                pt->upload(&shapes[s].idx, sh.indices, 3 * (size_t)sh.num_faces))
+                return cleanup(fail(PUPIL_ERR_OOM, "mesh upload failed"));
+        } else if (sh.kind != PUPIL_SHAPE_SPHERE) {
+            return cleanup(fail(PUPIL_ERR_INVALID, "unknown shape kind"));
+        }
+    }
+    // materials (optix_material.cpp:39-132 host precompute)
+    std::vector<DevMaterial> mats(scene->num_materials);
+    for (uint32_t m = 0; m < scene->num_materials; m++) {
+        const pupil_material &src = scene->materials[m];
+        DevMaterial &d = mats[m];
+        std::memset(&d, 0, sizeof(d));
+        d.type = src.type <= 7u ? src.type : 0u;
+        d.twosided = src.twosided;
+        d.nonlinear = src.nonlinear;
+        if (d.type == PUPIL_MAT_DIELECTRIC || d.type == PUPIL_MAT_ROUGH_DIELECTRIC || d.type == PUPIL_MAT_PLASTIC ||
+            d.type == PUPIL_MAT_ROUGH_PLASTIC)
+            d.eta = src.int_ior / src.ext_ior;
+        if (d.type == PUPIL_MAT_PLASTIC || d.type == PUPIL_MAT_ROUGH_PLASTIC) {
+            const pupil_texture &dt = d.type == PUPIL_MAT_PLASTIC ? src.tex[0] : src.tex[1];
+            const pupil_texture &stx = d.type == PUPIL_MAT_PLASTIC ? src.tex[1] : src.tex[2];
+            const float diffuse_luminance = luminance(pixel_average(dt));
+            const float specular_luminance = luminance(pixel_average(stx));
+            d.specular_sampling_weight = specular_luminance / (specular_luminance + diffuse_luminance);
+            d.int_fdr = diffuse_reflectance(1.f / d.eta);
+        }
+        for (int k = 0; k < 4; k++) {
+            int rc = upload_texture(pt, src.tex[k], d.tex[k]);
+            if (rc) return cleanup(rc);
+        }
+    }
+    if (mats.empty()) {  // keep a valid pointer for instances without material
+        DevMaterial d;
+        std::memset(&d, 0, sizeof(d));
+        mats.push_back(d);
+    }
+    // instances + primitive -> instance table
+    std::vector<DevInstance> insts(scene->num_instances);
+    std::vector<uint32_t> prim_inst;
+    for (uint32_t i = 0; i < scene->num_instances; i++) {
+        const pupil_instance &src = scene->instances[i];
+        if (src.shape >= scene->num_shapes) return cleanup(fail(PUPIL_ERR_INVALID, "instance shape out of range"));
+        if (src.material >= mats.size()) return cleanup(fail(PUPIL_ERR_INVALID, "instance material out of range"));
+        const pupil_shape &sh = scene->shapes[src.shape];
+        DevInstance &d = insts[i];
+        std::memset(&d, 0, sizeof(d));
+        std::memcpy(d.to_world, src.to_world, sizeof(d.to_world));
+        std::memcpy(d.to_object, src.to_object, sizeof(d.to_object));
+        d.kind = sh.kind;
+        d.material = src.material;
+        d.prim_offset = (uint32_t)prim_inst.size();
+        d.emitter_offset = src.emitter_offset;
+        d.flip_normals = src.flip_normals;
+        d.flip_tex_coords = src.flip_tex_coords;
+        d.positions = shapes[src.shape].pos;
+        d.normals = shapes[src.shape].nrm;
+        d.texcoords = shapes[src.shape].tex;
+        d.indices = shapes[src.shape].idx;
+        const uint32_t nprim = sh.kind == PUPIL_SHAPE_SPHERE ? 1u : sh.num_faces;
+        if (src.emitter_offset >= 0 && (size_t)src.emitter_offset + nprim > scene->num_area_emitters)
+            return cleanup(fail(PUPIL_ERR_INVALID, "emitter offset out of range"));
+        prim_inst.insert(prim_inst.end(), nprim, i);
+    }
+    pt->num_prims = (uint32_t)prim_inst.size();
+    if (pt->num_prims >= (1u << 28)) return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "more than 2^28 primitives"));
+    DevInstance *d_insts = nullptr;
+    DevMaterial *d_mats = nullptr;
+    uint32_t *d_prim_inst = nullptr;
+    if (pt->upload(&d_insts, insts.data(), insts.size()) || pt->upload(&d_mats, mats.data(), mats.size()) ||
+        pt->upload(&d_prim_inst, prim_inst.data(), prim_inst.size()))
+        return cleanup(fail(PUPIL_ERR_OOM, "scene upload failed"));
+    // emitters (EmitterGroup) + sequential selection CDF (emitter.h:110-120)
+    std::vector<DevEmitter> areas(scene->num_area_emitters);
+    std::vector<float> cdf(scene->num_area_emitters);
+    float sum_p = 0.f;
+    for (uint32_t e = 0; e < scene->num_area_emitters; e++) {
+        int rc = convert_emitter(pt, scene->area_emitters[e], areas[e]);
+        if (rc) return cleanup(rc);
+        cdf[e] = sum_p + areas[e].select_probability;
+        sum_p = cdf[e];
+    }
+    DevEmitter *d_areas = nullptr, *d_env = nullptr;
+    float *d_cdf = nullptr;
+    if (pt->upload(&d_areas, areas.data(), areas.size()) || pt->upload(&d_cdf, cdf.data(), cdf.size()))
+        return cleanup(fail(PUPIL_ERR_OOM, "emitter upload failed"));
+    if (scene->env && scene->env->type != PUPIL_EMITTER_NONE) {
+        DevEmitter env;
+        int rc = convert_emitter(pt, *scene->env, env);
+        if (rc) return cleanup(rc);
+        if (pt->upload(&d_env, &env, 1)) return cleanup(fail(PUPIL_ERR_OOM, "env upload failed"));
+    }
+    // LBVH (replaces GAS + IAS builds)
+    BvhBuildInput bin{pt->num_prims, d_prim_inst, d_insts, d_mats};
+    if (build_lbvh(bin, pt->bvh, 4u, pt->own_stream, &pt->build_ms) != 0)
+        return cleanup(fail(PUPIL_ERR_HIP, "LBVH build failed"));
+    DeviceScene &sc = pt->sc;
+    sc.nodes = pt->bvh.nodes;
+    sc.prims = pt->bvh.prims;
+    sc.num_prims = pt->num_prims;
+    sc.root_link = pt->bvh.root_link;
+    sc.prim_inst = d_prim_inst;
+    sc.instances = d_insts;
+    sc.materials = d_mats;
+    sc.areas = d_areas;
+    sc.area_cdf = d_cdf;
+    sc.num_areas = scene->num_area_emitters;
+    sc.has_env = d_env ? 1u : 0u;
+    sc.env = d_env;
+    std::memcpy(sc.camera.s2c, scene->sample_to_camera, sizeof(sc.camera.s2c));
+    std::memcpy(sc.camera.c2w, scene->camera_to_world, sizeof(sc.camera.c2w));
+    // traversal overflow stacks, counters, events
+    pt->ovf_threads = trace_grid_blocks() * (uint32_t)kTraceBlock;
+    if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 2) ||
+        pt->alloc(&pt->ray_log, 2 * 130) || pt->alloc(&pt->q.counts, 16))
+        return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
+    if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
+        return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
+    pt->totals.bvh_nodes = pt->bvh.num_nodes;
+    pt->totals.bvh_prims = pt->num_prims;
+    pt->totals.build_ms = pt->build_ms;
+    *out = pt;
+    return PUPIL_OK;
+}
+
+int pupil_pt_set_camera(pupil_pt *pt, const float sample_to_camera[16], const float camera_to_world[16]) {
+    if (!pt || !sample_to_camera || !camera_to_world) return fail(PUPIL_ERR_INVALID, "null argument");
+    std::memcpy(pt->sc.camera.s2c, sample_to_camera, sizeof(pt->sc.camera.s2c));
+    std::memcpy(pt->sc.camera.c2w, camera_to_world, sizeof(pt->sc.camera.c2w));
+    return PUPIL_OK;
+}
+
+int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_world[12], const float to_object[12]) {
+    (void)pt;
+    (void)instance;
+    (void)to_world;
+    (void)to_object;
+    return fail(PUPIL_ERR_UNSUPPORTED, "instance refit is not implemented yet (rebuild with pupil_pt_create)");
+}
+
+int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_launch *launch, void *hip_stream) {
+    if (!pt || !out || !launch || !out->accum) return fail(PUPIL_ERR_INVALID, "null argument");
+    if (launch->spp == 0) return PUPIL_OK;
+    const uint32_t world = launch->tile_world ? launch->tile_world : 1u;
+    const uint32_t ts = launch->tile_size ? launch->tile_size : 32u;
+    if (launch->tile_rank >= world) return fail(PUPIL_ERR_INVALID, "tile_rank >= tile_world");
+    HIP_TRY(hipSetDevice(pt->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : pt->own_stream;
+
+    // local pixel map (cached per tiling)
+    const uint32_t key[5] = {pt->width, pt->height, ts, launch->tile_rank, world};
+    const uint32_t *map = nullptr;
+    uint32_t num_local = pt->width * pt->height;
+    if (world > 1) {
+        if (!pt->pixel_map || std::memcmp(key, pt->pm_key, sizeof(key)) != 0) {
+            num_local = local_pixels(pt->width, pt->height, ts, launch->tile_rank, world, nullptr);
+            std::vector<uint32_t> host(num_local ? num_local : 1);
+            local_pixels(pt->width, pt->height, ts, launch->tile_rank, world, host.data());
+            if (pt->pixel_map) (void)hipFree(pt->pixel_map);
+            pt->pixel_map = nullptr;
+            HIP_TRY(hipMalloc((void **)&pt->pixel_map, sizeof(uint32_t) * host.size()));
+            HIP_TRY(hipMemcpy(pt->pixel_map, host.data(), sizeof(uint32_t) * host.size(), hipMemcpyHostToDevice));
+            std::memcpy(pt->pm_key, key, sizeof(key));
+            pt->pm_count = num_local;
+        }
+        map = pt->pixel_map;
+        num_local = pt->pm_count;
+    }
+    if (num_local == 0) return PUPIL_OK;
+    const size_t paths = (size_t)num_local * launch->spp;
+    if (paths >= (1ull << 31)) return fail(PUPIL_ERR_UNSUPPORTED, "too many paths in one batch");
+    int rc = ensure_state(pt, paths);
+    if (rc) return rc;
+
+    FrameParams fp{};
+    fp.width = pt->width;
+    fp.height = pt->height;
+    fp.num_local = num_local;
+    fp.num_paths = (uint32_t)paths;
+    fp.spp = launch->spp;
+    fp.seed0 = launch->random_seed;
+    fp.cnt0 = launch->sample_cnt;
+    fp.accumulate = launch->accumulate;
+    fp.max_depth = launch->max_depth ? launch->max_depth : pt->max_depth;
+    fp.compact = out->compact;
+    fp.pixel_map = map;
+    fp.accum = (float4 *)out->accum;
+    fp.frame = (float4 *)out->frame;
+    fp.albedo = (float *)out->albedo;
+    fp.normal = (float *)out->normal;
+    fp.test = (float *)out->test;
+
+    const bool stats = launch->collect_stats != 0;
+    TraceStats ts_dev{pt->trace_counters};
+    const TraceStats *tsp = stats ? &ts_dev : nullptr;
+    const uint32_t bounces = fp.max_depth;
+    // events: begin/end + one pair per trace launch
+    const uint32_t pairs_needed = 2 * bounces + 1;
+    while (pt->trace_events.size() < 2 * pairs_needed) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        pt->trace_events.push_back(e);
+    }
+    uint32_t pair = 0;
+    auto ev0 = [&]() { (void)hipEventRecord(pt->trace_events[2 * pair], s); };
+    auto ev1 = [&]() {
+        (void)hipEventRecord(pt->trace_events[2 * pair + 1], s);
+        pair++;
+    };
+
+    HIP_TRY(hipEventRecord(pt->ev_begin, s));
+    if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 2 * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(pt->ray_log, 0, sizeof(uint32_t) * 2 * 130, s));
+    launch_generate(pt->sc, fp, pt->ps, s);
+    HIP_TRY(hipMemsetAsync(pt->q.counts, 0, 16 * sizeof(uint32_t), s));
+    ev0();
+    launch_extend(pt->sc, pt->ps, pt->q, nullptr, nullptr, fp.num_paths, pt->ovf, pt->ovf_threads, tsp, s);
+    ev1();
+    for (uint32_t b = 0; b < bounces; b++) {
+        HIP_TRY(hipMemsetAsync(pt->q.counts + 9, 0, 2 * sizeof(uint32_t), s));
+        launch_shade(pt->sc, fp, pt->ps, pt->q, b, s);
+        if (b < 128)
+            HIP_TRY(hipMemcpyAsync(pt->ray_log + 2 * b, pt->q.counts + 9, 2 * sizeof(uint32_t),
+                                   hipMemcpyDeviceToDevice, s));
+        if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
+            ev0();
+            launch_shadow(pt->sc, pt->ps, pt->q, pt->ovf, pt->ovf_threads, tsp, s);
+            ev1();
+            HIP_TRY(hipMemsetAsync(pt->q.counts, 0, 9 * sizeof(uint32_t), s));
+            ev0();
+            launch_extend(pt->sc, pt->ps, pt->q, pt->q.next, pt->q.counts + 9, 0u, pt->ovf, pt->ovf_threads, tsp, s);
+            ev1();
+        }
+    }
+    launch_accumulate(fp, pt->ps, s);
+    HIP_TRY(hipEventRecord(pt->ev_end, s));
+    HIP_TRY(hipGetLastError());
+    pt->trace_pairs = pair;
+    pt->last_paths = fp.num_paths;
+    pt->last_bounces = bounces < 128 ? bounces : 128;
+    pt->last_stats = stats;
+    return PUPIL_OK;
+}
+
+int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
+    if (!pt || !out) return fail(PUPIL_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(pt->device));
+    HIP_TRY(hipEventSynchronize(pt->ev_end));
+    pupil_pt_counters c = pt->totals;
+    if (pt->last_paths) {
+        std::vector<uint32_t> log(2 * 130, 0);
+        HIP_TRY(hipMemcpy(log.data(), pt->ray_log, sizeof(uint32_t) * log.size(), hipMemcpyDeviceToHost));
+        c.primary_rays = pt->last_paths;
+        c.path_samples = pt->last_paths;
+        c.extension_rays = 0;
+        c.shadow_rays = 0;
+        for (uint32_t b = 0; b < pt->last_bounces; b++) {
+            c.extension_rays += log[2 * b];
+            c.shadow_rays += log[2 * b + 1];
+        }
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, pt->ev_begin, pt->ev_end));
+        c.last_render_ms = ms;
+        double tms = 0.0;
+        for (uint32_t i = 0; i < pt->trace_pairs; i++) {
+            float m = 0.f;
+            HIP_TRY(hipEventElapsedTime(&m, pt->trace_events[2 * i], pt->trace_events[2 * i + 1]));
+            tms += m;
+        }
+        c.trace_ms = tms;
+        c.trace_launches = pt->trace_pairs;
+        if (pt->last_stats) {
+            unsigned long long tc[2];
+            HIP_TRY(hipMemcpy(tc, pt->trace_counters, sizeof(tc), hipMemcpyDeviceToHost));
+            c.node_visits = tc[0];
+            c.prim_tests = tc[1];
+            const double rays = (double)(c.primary_rays + c.extension_rays + c.shadow_rays);
+            // 32 B ray read + 16 B hit write + 64 B per node + 48 B per primitive
+            c.trace_bytes = rays * 48.0 + 64.0 * (double)tc[0] + 48.0 * (double)tc[1];
+        }
+    }
+    *out = c;
+    return PUPIL_OK;
+}
+
+void pupil_pt_destroy(pupil_pt *pt) { delete pt; }
+
+int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out, int any_hit) {
+    if (!pt || !rays || !out) return fail(PUPIL_ERR_INVALID, "null argument");
+    if (n == 0) return PUPIL_OK;
+    HIP_TRY(hipSetDevice(pt->device));
+    float *d_rays = nullptr, *d_out = nullptr;
+    HIP_TRY(hipMalloc((void **)&d_rays, sizeof(float) * 8 * (size_t)n));
+    hipError_t e = hipMalloc((void **)&d_out, sizeof(float) * 4 * (size_t)n);
+    if (e == hipSuccess) e = hipMemcpy(d_rays, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        launch_trace_debug(pt->sc, d_rays, d_out, n, any_hit, pt->ovf, pt->ovf_threads, pt->own_stream);
+        e = hipStreamSynchronize(pt->own_stream);
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(float) * 4 * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_rays);
+    if (d_out) (void)hipFree(d_out);
+    HIP_TRY(e);
+    return PUPIL_OK;
+}
+
+int pupil_debug_math(int device, uint32_t n, const float *x, const float *y2, float *out) {
+    if (!x || !y2 || !out) return fail(PUPIL_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(device));
+    float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    HIP_TRY(hipMalloc((void **)&dx, sizeof(float) * (n ? n : 1)));
+    HIP_TRY(hipMalloc((void **)&dy, sizeof(float) * (n ? n : 1)));
+    HIP_TRY(hipMalloc((void **)&dout, sizeof(float) * 6 * (n ? n : 1)));
+    HIP_TRY(hipMemcpy(dx, x, sizeof(float) * n, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dy, y2, sizeof(float) * n, hipMemcpyHostToDevice));
+    launch_debug_math(dx, dy, dout, n, nullptr);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, dout, sizeof(float) * 6 * n, hipMemcpyDeviceToHost));
+    (void)hipFree(dx);
+    (void)hipFree(dy);
+    (void)hipFree(dout);
+    return PUPIL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// pt_kernels.h — host-visible declarations of the wavefront stages and the
+// LBVH builder (implemented in pt_kernels.hip / bvh_build.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "pt_scene.h"
+
+namespace pupil {
+
+constexpr int kTraceBlock = 128;
+constexpr int kStackLds = 32;   // per-thread LDS stack entries
+constexpr int kStackOvf = 64;   // per-thread global overflow entries
+constexpr int kShadeBlock = 256;
+constexpr uint32_t kNumQueues = 9;  // 0 = miss, 1..7 = EMatType, 8 = unknown material
+constexpr uint32_t kMissIndex = 0xFFFFFFFFu;
+
+// Path state in HBM, structure of arrays indexed by path id
+// p = sample * num_local_pixels + local_pixel.
+struct PathState {
+    float4 *ray_o;      // xyz origin of the current ray
+    float4 *ray_d;      // xyz direction
+    float4 *hit;        // t, b1, b2, sorted primitive index (bits) or kMissIndex
+    float4 *thr;        // xyz throughput, w = pdf of the BSDF sample that spawned the ray
+    float4 *rad;        // xyz radiance
+    uint4 *misc;        // x rng, y bounce | delta<<8, z/w texcoord (stale semantics, geometry.h:298-304)
+    float4 *sh_o;       // shadow ray origin, w = tmax
+    float4 *sh_d;       // shadow ray direction
+    float4 *sh_c;       // pending NEE contribution
+};
+
+struct Queues {
+    uint32_t *bins;      // kNumQueues * capacity
+    uint32_t *next;      // capacity
+    uint32_t *shadow;    // capacity
+    uint32_t *counts;    // [0..8] bins, [9] next, [10] shadow
+    uint32_t capacity;
+};
+
+struct FrameParams {
+    uint32_t width, height;
+    uint32_t num_local;    // local pixels
+    uint32_t num_paths;    // num_local * spp
+    uint32_t spp;
+    uint32_t seed0;
+    uint32_t cnt0;
+    uint32_t accumulate;
+    uint32_t max_depth;
+    uint32_t compact;
+    const uint32_t *pixel_map;  // local -> global pixel (null = identity)
+    float4 *accum;
+    float4 *frame;
+    float *albedo;  // 3 floats per pixel
+    float *normal;
+    float *test;
+};
+
+struct TraceStats {
+    unsigned long long *counters;  // [0] nodes, [1] prims
+};
+
+// wavefront stages
+void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, hipStream_t s);
+void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
+                   const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
+                   const TraceStats *stats, hipStream_t s);
+void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,
+                  uint32_t bounce, hipStream_t s);
+void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
+                   const TraceStats *stats, hipStream_t s);
+void launch_accumulate(const FrameParams &fp, const PathState &ps, hipStream_t s);
+uint32_t trace_grid_blocks();
+void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
+                        uint32_t ovf_threads, hipStream_t s);
+void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, hipStream_t s);
+
+// LBVH builder (bvh_build.hip)
+struct BvhBuildInput {
+    uint32_t num_prims;
+    const uint32_t *prim_inst;      // device, global prim -> instance
+    const DevInstance *instances;   // device
+    const DevMaterial *materials;   // device
+};
+struct BvhBuildOutput {
+    BvhNode *nodes;     // device, max(1, n-1)
+    float4 *prims;      // device, 3 * n
+    uint32_t root_link;
+    uint32_t num_nodes;
+};
+int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms);
+void free_lbvh(BvhBuildOutput &out);
+
+}  // namespace pupil

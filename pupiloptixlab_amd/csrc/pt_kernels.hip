@@ -1,0 +1,667 @@
+// pt_kernels.hip — the wavefront path tracer on gfx950.
+//
+// One frame batch = `spp` consecutive frames of PTPass::OnRun
+// (example/path_tracer/pt_pass.cpp:39-57) over the rank's pixels.  The
+// reference's per-pixel megakernel (__raygen__main, main.cu:36-194) is cut at
+// every optixTrace into stages that each run over a compacted queue:
+//
+//   generate  (main.cu:44-75)   camera ray + RNG init for every path
+//   extend    (main.cu:77,158)  closest hit; bins the path by material type
+//   shade<M>  (main.cu:84-183)  one kernel per EMatType: hit reconstruction,
+//                               emission/MIS, RR, NEE sample + BSDF eval,
+//                               BSDF sample -> shadow queue + next queue
+//   shadow    (main.cu:119-140) any hit; adds the pending NEE contribution
+//   accumulate(main.cu:185-193) running-mean over the batch's frames, in order
+//
+// Every float operation of the reference is reproduced in the same order, so
+// a path gives bit-identical radiance to the reference-order CPU oracle.
+#include "pt_kernels.h"
+#include "pt_shading.h"
+#include "pt_trace.h"
+
+namespace pupil {
+
+namespace {
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// Wave-aggregated append: one atomic per wave per queue (wave-ballot prefix sum).
+__device__ __forceinline__ void wave_append(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
+    const unsigned long long m = __ballot(pred);
+    if (m == 0ull) return;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (pred) queue[base + (uint32_t)__popcll(m & lanemask_lt())] = value;
+}
+
+__device__ __forceinline__ vec3 f3(float4 v) { return v3(v.x, v.y, v.z); }
+__device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
+
+// ------------------------------------------------------------------ traversal
+// Stack: kStackLds entries in LDS (lane-interleaved), overflow to HBM.
+struct Stack {
+    int *lds;          // this thread's column base
+    int *ovf;          // this thread's overflow base
+    uint32_t ovf_stride;
+    __device__ __forceinline__ void store(int i, int v) {
+        if (i < kStackLds) lds[i * kTraceBlock] = v;
+        else ovf[(size_t)(i - kStackLds) * ovf_stride] = v;
+    }
+    __device__ __forceinline__ int load(int i) const {
+        return i < kStackLds ? lds[i * kTraceBlock] : ovf[(size_t)(i - kStackLds) * ovf_stride];
+    }
+};
+
+constexpr int kSentinel = 0x76543210;
+
+// Aila-Laine while-while traversal with postponed leaves.  ANY = shadow
+// (terminate on first hit, OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT).
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool traverse(const DeviceScene &sc, const RayPre &r, float tmin, float &tmax,
+                                         uint32_t &best_key, uint32_t &best_idx, float &bb1, float &bb2, Stack &st,
+                                         uint32_t &nodes_visited, uint32_t &prims_tested) {
+    int sp = 0;
+    st.store(0, kSentinel);
+    int node = (int)sc.root_link;
+    int leaf = 0;
+    bool found = false;
+    while (node != kSentinel) {
+        while ((uint32_t)node < (uint32_t)kSentinel) {
+            const BvhNode n = sc.nodes[node];
+            if (STATS) nodes_visited++;
+            const float t0 = box_entry(r, v3(n.lo0.x, n.lo0.y, n.lo0.z), v3(n.hi0.x, n.hi0.y, n.hi0.z), tmin, tmax);
+            const float t1 = box_entry(r, v3(n.lo1.x, n.lo1.y, n.lo1.z), v3(n.hi1.x, n.hi1.y, n.hi1.z), tmin, tmax);
+            const bool h0 = t0 != __builtin_huge_valf();
+            const bool h1 = t1 != __builtin_huge_valf();
+            int c0 = __float_as_int(n.lo0.w);
+            int c1 = __float_as_int(n.hi0.w);
+            if (!h0 && !h1) {
+                node = st.load(sp);
+                sp--;
+            } else {
+                node = h0 ? c0 : c1;
+                if (h0 && h1) {
+                    if (t1 < t0) {
+                        const int tmp = node;
+                        node = c1;
+                        c1 = tmp;
+                    }
+                    sp++;
+                    if (sp >= kStackLds + kStackOvf) sp = kStackLds + kStackOvf - 1;  // never reached (depth <= 62)
+                    st.store(sp, c1);
+                }
+            }
+            if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
+                leaf = node;
+                node = st.load(sp);
+                sp--;
+            }
+            if (!__any(leaf >= 0)) break;
+        }
+        while (leaf < 0) {
+            const uint32_t first = leaf_first(leaf);
+            const uint32_t count = leaf_count(leaf);
+            for (uint32_t i = first; i < first + count; i++) {
+                const float4 a = sc.prims[3 * i + 0];
+                const uint32_t ref = __float_as_uint(a.w);
+                const uint32_t key = ref & ~kPrimSphereBit;
+                if (STATS) prims_tested++;
+                float t, b1 = 0.f, b2 = 0.f;
+                bool hit;
+                if (ref & kPrimSphereBit) {
+                    const float4 b = sc.prims[3 * i + 1];
+                    const DevInstance &in = sc.instances[__float_as_uint(b.w)];
+                    hit = intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, t);
+                } else {
+                    const float4 b = sc.prims[3 * i + 1];
+                    const float4 c = sc.prims[3 * i + 2];
+                    hit = intersect_triangle(r, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), tmin, tmax, t,
+                                             b1, b2);
+                }
+                if (hit) {
+                    if (ANY) {
+                        found = true;
+                        break;
+                    }
+                    if (t < tmax || key < best_key) {
+                        tmax = t;
+                        best_key = key;
+                        best_idx = i;
+                        bb1 = b1;
+                        bb2 = b2;
+                        found = true;
+                    }
+                }
+            }
+            if (ANY && found) break;
+            leaf = node;
+            if (node < 0) {
+                node = st.load(sp);
+                sp--;
+            }
+        }
+        if (ANY && found) break;
+    }
+    return found;
+}
+
+template <bool STATS>
+__device__ __forceinline__ void flush_stats(const TraceStats *stats, uint32_t nv, uint32_t pt) {
+    if (!STATS) return;
+    // wave reduction then one atomic per wave
+    unsigned long long a = nv, b = pt;
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o);
+        b += __shfl_xor(b, o);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(&stats->counters[0], a);
+        atomicAdd(&stats->counters[1], b);
+    }
+}
+
+// ------------------------------------------------------------------ extend
+template <bool STATS>
+__global__ __launch_bounds__(kTraceBlock) void k_extend(DeviceScene sc, PathState ps, Queues q,
+                                                        const uint32_t *queue, const uint32_t *queue_count,
+                                                        uint32_t static_count, int *ovf, uint32_t ovf_threads,
+                                                        TraceStats stats) {
+    __shared__ int s_stack[kStackLds * kTraceBlock];
+    const uint32_t count = queue_count ? *queue_count : static_count;
+    Stack st;
+    st.lds = s_stack + threadIdx.x;
+    const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    st.ovf = ovf + gtid;
+    st.ovf_stride = ovf_threads;
+    uint32_t nv = 0, pt = 0;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    // whole waves iterate together so wave_append sees every lane
+    const uint32_t wave_base = (blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
+    for (uint32_t base = wave_base; base < count; base += stride) {
+        const uint32_t i = base + lane_id();
+        const bool valid = i < count;
+        uint32_t p = 0;
+        uint32_t bin = 0;
+        if (valid) {
+            p = queue ? queue[i] : i;
+            const float4 o = ps.ray_o[p];
+            const float4 d = ps.ray_d[p];
+            const RayPre r = ray_pre(f3(o), f3(d));
+            float tmax = kMaxDistance;
+            uint32_t best_key = 0xFFFFFFFFu, best_idx = kMissIndex;
+            float b1 = 0.f, b2 = 0.f;
+            const bool hit = traverse<false, STATS>(sc, r, 0.001f, tmax, best_key, best_idx, b1, b2, st, nv, pt);
+            ps.hit[p] = make_float4(hit ? tmax : -1.f, b1, b2, __uint_as_float(hit ? best_idx : kMissIndex));
+            if (hit) {
+                const uint32_t mt = __float_as_uint(sc.prims[3 * best_idx + 2].w);
+                bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
+            }
+        }
+        // bin by material: loop over the distinct bins present in the wave
+        bool pending = valid;
+        while (__any(pending)) {
+            const unsigned long long m = __ballot(pending);
+            const int leader = __ffsll((long long)m) - 1;
+            const uint32_t b = __shfl(bin, leader);
+            const bool mine = pending && bin == b;
+            wave_append(mine, p, q.bins + (size_t)b * q.capacity, q.counts + b);
+            if (mine) pending = false;
+        }
+    }
+    flush_stats<STATS>(&stats, nv, pt);
+}
+
+// ------------------------------------------------------------------ shadow
+template <bool STATS>
+__global__ __launch_bounds__(kTraceBlock) void k_shadow(DeviceScene sc, PathState ps, Queues q, int *ovf,
+                                                        uint32_t ovf_threads, TraceStats stats) {
+    __shared__ int s_stack[kStackLds * kTraceBlock];
+    const uint32_t count = q.counts[10];
+    Stack st;
+    st.lds = s_stack + threadIdx.x;
+    const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    st.ovf = ovf + gtid;
+    st.ovf_stride = ovf_threads;
+    uint32_t nv = 0, pt = 0;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = gtid; i < count; i += stride) {
+        const uint32_t p = q.shadow[i];
+        const float4 o = ps.sh_o[p];
+        const float4 d = ps.sh_d[p];
+        const RayPre r = ray_pre(f3(o), f3(d));
+        float tmax = o.w;
+        uint32_t k = 0, idx = 0;
+        float b1, b2;
+        const bool occluded = traverse<true, STATS>(sc, r, 0.001f, tmax, k, idx, b1, b2, st, nv, pt);
+        if (!occluded) {  // main.cu:124-139
+            const float4 c = ps.sh_c[p];
+            float4 L = ps.rad[p];
+            L.x = L.x + c.x;
+            L.y = L.y + c.y;
+            L.z = L.z + c.z;
+            ps.rad[p] = L;
+        }
+    }
+    flush_stats<STATS>(&stats, nv, pt);
+}
+
+// ------------------------------------------------------------------ generate
+__device__ __forceinline__ uint32_t global_pixel(const FrameParams &fp, uint32_t l) {
+    return fp.pixel_map ? fp.pixel_map[l] : l;
+}
+
+__global__ __launch_bounds__(kShadeBlock) void k_generate(DeviceScene sc, FrameParams fp, PathState ps) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= fp.num_paths) return;
+    const uint32_t s = p / fp.num_local;
+    const uint32_t l = p - s * fp.num_local;
+    const uint32_t pixel = global_pixel(fp, l);
+    const uint32_t y = pixel / fp.width;
+    const uint32_t x = pixel - y * fp.width;
+    uint32_t rng = rng_init(pixel, fp.seed0 + s);  // main.cu:53
+    const float jx = rng_next(rng);                 // main.cu:55 (x drawn first)
+    const float jy = rng_next(rng);
+    const vec4 film = v4(((float)x + jx) / (float)fp.width, ((float)y + jy) / (float)fp.height, 0.f, 1.f);
+    const float *m = sc.camera.s2c;
+    vec4 d = v4(dot(v4(m[0], m[1], m[2], m[3]), film), dot(v4(m[4], m[5], m[6], m[7]), film),
+                dot(v4(m[8], m[9], m[10], m[11]), film), dot(v4(m[12], m[13], m[14], m[15]), film));
+    const float inv_w = 1.0f / d.w;
+    d = v4(d.x * inv_w, d.y * inv_w, d.z * inv_w, d.w * inv_w);
+    d.w = 0.f;
+    d = normalize(d);
+    const float *c = sc.camera.c2w;
+    const vec3 dir = normalize(v3(dot(v4(c[0], c[1], c[2], c[3]), d), dot(v4(c[4], c[5], c[6], c[7]), d),
+                                  dot(v4(c[8], c[9], c[10], c[11]), d)));
+    ps.ray_o[p] = make_float4(c[3], c[7], c[11], 0.f);
+    ps.ray_d[p] = make_float4(dir.x, dir.y, dir.z, 0.f);
+    ps.thr[p] = make_float4(1.f, 1.f, 1.f, 0.f);
+    ps.rad[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+    ps.misc[p] = make_uint4(rng, 0u, 0u, 0u);
+}
+
+// ------------------------------------------------------------------ shade
+struct HitGeo {
+    LocalGeo g;
+    int emitter;
+    uint32_t inst;
+};
+
+// __closesthit__default (main.cu:216-230) + Geometry::GetHitLocalGeometry
+// (render/geometry.h:272-320), from the compact hit record.
+__device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, vec3 ro, vec3 rd, vec2 stale_uv) {
+    HitGeo out;
+    const uint32_t idx = __float_as_uint(h.w);
+    const float4 a = sc.prims[3 * idx + 0];
+    const float4 b = sc.prims[3 * idx + 1];
+    const uint32_t ref = __float_as_uint(a.w);
+    const uint32_t gprim = ref & ~kPrimSphereBit;
+    const uint32_t inst_id = __float_as_uint(b.w);
+    const DevInstance &in = sc.instances[inst_id];
+    out.inst = inst_id;
+    LocalGeo &g = out.g;
+    g.texcoord = stale_uv;
+    uint32_t local = 0;
+    if (ref & kPrimSphereBit) {
+        g.position = ro + h.x * rd;
+        const vec3 local_pos = xform_point(in.to_object, g.position);
+        g.texcoord = sphere_texcoord(normalize(local_pos - v3(0.f)));
+        g.normal = normalize(xform_normal(in.to_object, local_pos - v3(0.f)));
+        if (in.flip_normals) g.normal = g.normal * -1.f;
+    } else {
+        local = gprim - in.prim_offset;
+        const uint32_t i0 = in.indices[3 * local + 0], i1 = in.indices[3 * local + 1], i2 = in.indices[3 * local + 2];
+        const float *P = in.positions;
+        const vec3 p0 = v3(P[3 * i0], P[3 * i0 + 1], P[3 * i0 + 2]);
+        const vec3 p1 = v3(P[3 * i1], P[3 * i1 + 1], P[3 * i1 + 2]);
+        const vec3 p2 = v3(P[3 * i2], P[3 * i2 + 1], P[3 * i2 + 2]);
+        const float u = h.y, v = h.z;
+        const float w = 1.f - u - v;
+        g.position = w * p0 + u * p1 + v * p2;
+        g.position = xform_point(in.to_world, g.position);
+        vec3 n;
+        if (in.normals) {
+            const float *N = in.normals;
+            const vec3 n0 = v3(N[3 * i0], N[3 * i0 + 1], N[3 * i0 + 2]);
+            const vec3 n1 = v3(N[3 * i1], N[3 * i1 + 1], N[3 * i1 + 2]);
+            const vec3 n2 = v3(N[3 * i2], N[3 * i2 + 1], N[3 * i2 + 2]);
+            n = w * n0 + u * n1 + v * n2;
+        } else {
+            n = cross(p1 - p0, p2 - p0);
+        }
+        g.normal = normalize(xform_normal(in.to_object, n));
+        if (in.flip_normals) g.normal = g.normal * -1.f;
+        if (in.texcoords) {
+            const float *T = in.texcoords;
+            const vec2 t0 = v2(T[2 * i0], T[2 * i0 + 1]);
+            const vec2 t1 = v2(T[2 * i1], T[2 * i1 + 1]);
+            const vec2 t2 = v2(T[2 * i2], T[2 * i2 + 1]);
+            g.texcoord = w * t0 + u * t1 + v * t2;
+            if (in.flip_tex_coords) g.texcoord.y = 1.f - g.texcoord.y;
+        }
+    }
+    out.emitter = in.emitter_offset >= 0 ? in.emitter_offset + (int)local : -1;
+    return out;
+}
+
+// EmitterGroup::SelectOneEmiiter (render/emitter.h:110-135) as a binary search
+// over the sequentially accumulated CDF: picks the same emitter as the scan.
+__device__ __forceinline__ const DevEmitter *select_emitter(const DeviceScene &sc, float p, float &sel_prob) {
+    uint32_t lo = 0, hi = sc.num_areas;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (p <= sc.area_cdf[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    const DevEmitter *e = nullptr;
+    if (lo < sc.num_areas) e = &sc.areas[lo];
+    else if (sc.has_env) e = sc.env;
+    else if (sc.num_areas > 0) e = &sc.areas[sc.num_areas - 1];
+    sel_prob = e ? e->select_probability : 0.f;
+    return e;
+}
+
+template <uint32_t MAT>
+__global__ __launch_bounds__(kShadeBlock) void k_shade(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
+                                                       uint32_t bounce) {
+    const uint32_t bin = MAT == 0u ? 8u : MAT;
+    const uint32_t count = q.counts[bin];
+    const uint32_t *queue = q.bins + (size_t)bin * q.capacity;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t wave_base = (blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
+    for (uint32_t base = wave_base; base < count; base += stride) {
+        const uint32_t i = base + lane_id();
+        const bool valid = i < count;
+        bool push_next = false, push_shadow = false;
+        uint32_t p = 0;
+        if (valid) {
+            p = queue[i];
+            const uint32_t s = p / fp.num_local;
+            const uint32_t l = p - s * fp.num_local;
+            const float4 h = ps.hit[p];
+            const float4 o4 = ps.ray_o[p];
+            const float4 d4 = ps.ray_d[p];
+            const vec3 ray_o = f3(o4), ray_d = f3(d4);
+            uint4 misc = ps.misc[p];
+            uint32_t rng = misc.x;
+            const uint32_t flags = misc.y;
+            float4 thr4 = ps.thr[p];
+            vec3 T = f3(thr4);
+            const float prev_pdf = thr4.w;
+            float4 rad4 = ps.rad[p];
+            vec3 L = f3(rad4);
+            const vec2 stale_uv = v2(__uint_as_float(misc.z), __uint_as_float(misc.w));
+
+            HitGeo hg = reconstruct(sc, h, ray_o, ray_d, stale_uv);
+            const DevInstance &in = sc.instances[hg.inst];
+            const DevMaterial &mat = sc.materials[in.material];
+            if (mat.twosided && dot(-ray_d, hg.g.normal) < 0.f) hg.g.normal = -hg.g.normal;  // geometry.h:316-320
+            const LocalGeo &geo = hg.g;
+            LocalBsdf bsdf = local_bsdf(mat, geo.texcoord);
+            bsdf.type = MAT;
+
+            bool alive = true;
+            if (bounce == 0) {
+                if (hg.emitter >= 0) L = L + emitter_radiance(sc.areas[hg.emitter], geo.texcoord);  // main.cu:88-92
+                const float test = rng_next(rng);                                                    // main.cu:101
+                if (s + 1 == fp.spp) {
+                    const uint32_t out = fp.compact ? l : global_pixel(fp, l);
+                    if (fp.albedo) {
+                        const vec3 al = bsdf_albedo(bsdf);
+                        fp.albedo[3 * out + 0] = al.x;
+                        fp.albedo[3 * out + 1] = al.y;
+                        fp.albedo[3 * out + 2] = al.z;
+                    }
+                    if (fp.normal) {
+                        fp.normal[3 * out + 0] = geo.normal.x;
+                        fp.normal[3 * out + 1] = geo.normal.y;
+                        fp.normal[3 * out + 2] = geo.normal.z;
+                    }
+                    if (fp.test) fp.test[out] = test;
+                }
+            } else if (hg.emitter >= 0) {  // main.cu:171-182
+                const DevEmitter &e = sc.areas[hg.emitter];
+                vec3 Le;
+                float pdf_e;
+                emitter_eval_area(e, geo, ray_o, Le, pdf_e);
+                if (!is_zero(pdf_e)) {
+                    const float mis = (flags >> 8) & 1u ? 1.f : mis_weight(prev_pdf, pdf_e * e.select_probability);
+                    L = L + T * Le * mis;
+                }
+            }
+
+            // loop head (main.cu:103-111)
+            const uint32_t depth = bounce + 1;
+            if (depth >= fp.max_depth) alive = false;
+            if (alive) {
+                const float rr = depth > 2 ? 0.95f : 1.0f;
+                if (rng_next(rng) > rr) alive = false;
+                else T = T / rr;
+            }
+            float pdf_b = 0.f;
+            uint32_t delta = 0;
+            if (alive) {
+                // direct light sampling (main.cu:114-141)
+                float sel_prob;
+                const DevEmitter *e = select_emitter(sc, rng_next(rng), sel_prob);
+                const float x0 = rng_next(rng);
+                const float x1 = rng_next(rng);
+                const vec3 wo = to_local(-ray_d, geo.normal);
+                if (e) {
+                    const EmitterSample es = emitter_sample_direct(*e, geo, v2(x0, x1));
+                    BsdfRec er;
+                    er.wi = to_local(es.wi, geo.normal);
+                    er.wo = wo;
+                    er.f = v3(0.f);
+                    er.pdf = 0.f;
+                    bsdf_eval_t<MAT>(bsdf, er);
+                    if (!is_zero(er.f * es.pdf)) {
+                        const float NoL = dot(geo.normal, es.wi);
+                        if (NoL > 0.f) {
+                            const float mis = mis_weight(es.pdf, er.pdf);
+                            const float pdf_l = es.pdf * sel_prob;
+                            const vec3 C = T * es.radiance * er.f * NoL * mis / pdf_l;
+                            ps.sh_o[p] = f4(geo.position, es.distance - 0.001f);
+                            ps.sh_d[p] = f4(es.wi, 0.f);
+                            ps.sh_c[p] = f4(C, 0.f);
+                            push_shadow = true;
+                        }
+                    }
+                }
+                // BSDF sampling (main.cu:143-163)
+                BsdfRec br;
+                br.wo = wo;
+                br.wi = v3(0.f);
+                br.f = v3(0.f);
+                br.pdf = 0.f;
+                br.sampled_type = 0;
+                bsdf_sample_t<MAT>(bsdf, br, rng);
+                if (is_zero(br.f * fabs_(br.wi.z)) || is_zero(br.pdf)) {
+                    alive = false;
+                } else {
+                    T = T * (br.f * fabs_(br.wi.z) / br.pdf);
+                    const vec3 nd = to_world(br.wi, geo.normal);
+                    ps.ray_o[p] = f4(geo.position, 0.f);
+                    ps.ray_d[p] = f4(nd, 0.f);
+                    pdf_b = br.pdf;
+                    delta = (br.sampled_type & kLobeDelta) ? 1u : 0u;
+                    push_next = true;
+                }
+            }
+            ps.thr[p] = f4(T, pdf_b);
+            ps.rad[p] = f4(L, 0.f);
+            ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 8), __float_as_uint(geo.texcoord.x),
+                                    __float_as_uint(geo.texcoord.y));
+        }
+        wave_append(push_shadow, p, q.shadow, q.counts + 10);
+        wave_append(push_next, p, q.next, q.counts + 9);
+    }
+}
+
+// Paths whose ray left the scene (__miss__default, main.cu:196-212, and the
+// env handling at main.cu:87-99 / 165-169).
+__global__ __launch_bounds__(kShadeBlock) void k_shade_miss(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
+                                                            uint32_t bounce) {
+    const uint32_t count = q.counts[0];
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        const uint32_t p = q.bins[i];
+        if (bounce == 0) {
+            const uint32_t s = p / fp.num_local;
+            const uint32_t l = p - s * fp.num_local;
+            float4 rad4 = ps.rad[p];
+            vec3 L = f3(rad4);
+            uint32_t rng = ps.misc[p].x;
+            if (sc.has_env) {
+                vec3 Le;
+                float pdf;
+                env_eval(*sc.env, f3(ps.ray_o[p]), f3(ps.ray_d[p]), Le, pdf);
+                L = L + Le;  // main.cu:185, no MIS on the camera ray
+            }
+            const float test = rng_next(rng);
+            if (s + 1 == fp.spp) {
+                const uint32_t out = fp.compact ? l : global_pixel(fp, l);
+                if (fp.albedo) fp.albedo[3 * out] = fp.albedo[3 * out + 1] = fp.albedo[3 * out + 2] = 0.f;
+                if (fp.normal) fp.normal[3 * out] = fp.normal[3 * out + 1] = fp.normal[3 * out + 2] = 0.f;
+                if (fp.test) fp.test[out] = test;
+            }
+            ps.rad[p] = f4(L, 0.f);
+        } else if (sc.has_env) {
+            const float4 thr4 = ps.thr[p];
+            vec3 Le;
+            float env_pdf;
+            env_eval(*sc.env, f3(ps.ray_o[p]), f3(ps.ray_d[p]), Le, env_pdf);
+            const float mis = mis_weight(thr4.w, env_pdf);  // main.cu:166-167
+            const vec3 env_rad = Le * (f3(thr4) * mis);
+            float4 rad4 = ps.rad[p];
+            ps.rad[p] = f4(f3(rad4) + env_rad, 0.f);  // main.cu:185
+        }
+    }
+}
+
+// ------------------------------------------------------------------ accumulate
+__global__ __launch_bounds__(kShadeBlock) void k_accumulate(FrameParams fp, PathState ps) {
+    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= fp.num_local) return;
+    const uint32_t out = fp.compact ? l : global_pixel(fp, l);
+    vec3 acc = f3(fp.accum[out]);
+    for (uint32_t s = 0; s < fp.spp; s++) {
+        vec3 L = f3(ps.rad[(size_t)s * fp.num_local + l]);
+        const uint32_t cnt = fp.cnt0 + (fp.accumulate ? s : 0u);
+        if (fp.accumulate && cnt > 0) {  // main.cu:187-191
+            const float t = 1.f / ((float)cnt + 1.f);
+            L = lerp(acc, L, t);
+        }
+        acc = L;
+    }
+    fp.accum[out] = f4(acc, 1.f);
+    if (fp.frame) fp.frame[out] = f4(acc, 1.f);
+}
+
+// ------------------------------------------------------------------ verification kernels
+__global__ __launch_bounds__(kTraceBlock) void k_trace_debug(DeviceScene sc, const float *rays, float *out,
+                                                             uint32_t n, int any, int *ovf, uint32_t ovf_threads) {
+    __shared__ int s_stack[kStackLds * kTraceBlock];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Stack st;
+    st.lds = s_stack + threadIdx.x;
+    st.ovf = ovf + (i % ovf_threads);
+    st.ovf_stride = ovf_threads;
+    const float *r8 = rays + 8 * (size_t)i;
+    const RayPre r = ray_pre(v3(r8[0], r8[1], r8[2]), v3(r8[3], r8[4], r8[5]));
+    float tmax = r8[7];
+    uint32_t key = 0xFFFFFFFFu, idx = kMissIndex, nv = 0, pt = 0;
+    float b1 = 0.f, b2 = 0.f;
+    bool hit;
+    if (any) hit = traverse<true, false>(sc, r, r8[6], tmax, key, idx, b1, b2, st, nv, pt);
+    else hit = traverse<false, false>(sc, r, r8[6], tmax, key, idx, b1, b2, st, nv, pt);
+    float *o = out + 4 * (size_t)i;
+    o[0] = hit ? (any ? 1.f : tmax) : -1.f;
+    o[1] = b1;
+    o[2] = b2;
+    o[3] = __uint_as_float(hit && !any ? key : 0xFFFFFFFFu);
+}
+
+__global__ void k_debug_math(const float *x, const float *y2, float *out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float a = x[i], b = y2[i];
+    float s, c;
+    dm_sincos(a, s, c);
+    out[6 * i + 0] = s;
+    out[6 * i + 1] = c;
+    out[6 * i + 2] = dm_acos(fminf(fmaxf(a, -1.f), 1.f));
+    out[6 * i + 3] = dm_atan2(a, b);
+    out[6 * i + 4] = sqrtf(fabs_(a));
+    out[6 * i + 5] = 1.0f / a;
+}
+
+}  // namespace
+
+void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
+                        uint32_t ovf_threads, hipStream_t s) {
+    hipLaunchKernelGGL(k_trace_debug, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, s, sc, rays,
+                       out, n, any, ovf, ovf_threads);
+}
+
+void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_debug_math, dim3((n + 255) / 256), dim3(256), 0, s, x, y2, out, n);
+}
+
+// ------------------------------------------------------------------ launchers
+uint32_t trace_grid_blocks() { return 256u * 16u; }
+
+void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, hipStream_t s) {
+    const uint32_t blocks = (fp.num_paths + kShadeBlock - 1) / kShadeBlock;
+    hipLaunchKernelGGL(k_generate, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps);
+}
+
+void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
+                   const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
+                   const TraceStats *stats, hipStream_t s) {
+    const uint32_t blocks = ovf_threads / kTraceBlock;
+    TraceStats st = stats ? *stats : TraceStats{nullptr};
+    if (stats)
+        hipLaunchKernelGGL(k_extend<true>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, queue, queue_count,
+                           static_count, ovf, ovf_threads, st);
+    else
+        hipLaunchKernelGGL(k_extend<false>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, queue, queue_count,
+                           static_count, ovf, ovf_threads, st);
+}
+
+void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
+                   const TraceStats *stats, hipStream_t s) {
+    const uint32_t blocks = ovf_threads / kTraceBlock;
+    TraceStats st = stats ? *stats : TraceStats{nullptr};
+    if (stats)
+        hipLaunchKernelGGL(k_shadow<true>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, ovf, ovf_threads, st);
+    else
+        hipLaunchKernelGGL(k_shadow<false>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, ovf, ovf_threads, st);
+}
+
+void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,
+                  uint32_t bounce, hipStream_t s) {
+    const uint32_t blocks = 256u * 8u;
+    hipLaunchKernelGGL(k_shade_miss, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
+    hipLaunchKernelGGL(k_shade<PUPIL_MAT_DIFFUSE>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
+    hipLaunchKernelGGL(k_shade<PUPIL_MAT_DIELECTRIC>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
+    hipLaunchKernelGGL(k_shade<PUPIL_MAT_ROUGH_DIELECTRIC>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q,
+                       bounce);
+    hipLaunchKernelGGL(k_shade<PUPIL_MAT_CONDUCTOR>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
+    hipLaunchKernelGGL(k_shade<PUPIL_MAT_ROUGH_CONDUCTOR>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q,
+                       bounce);
+    hipLaunchKernelGGL(k_shade<PUPIL_MAT_PLASTIC>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
+    hipLaunchKernelGGL(k_shade<PUPIL_MAT_ROUGH_PLASTIC>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q,
+                       bounce);
+    hipLaunchKernelGGL(k_shade<0u>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
+}
+
+void launch_accumulate(const FrameParams &fp, const PathState &ps, hipStream_t s) {
+    const uint32_t blocks = (fp.num_local + kShadeBlock - 1) / kShadeBlock;
+    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kShadeBlock), 0, s, fp, ps);
+}
+
+}  // namespace pupil

@@ -1,0 +1,120 @@
+// pt_scene.h — device-resident scene layout of the MI355X path tracer.
+//
+// Everything the wavefront kernels read lives in one POD struct (DeviceScene)
+// passed by value as a kernel argument.  Layout choices (HBM-first):
+//   * BVH nodes: 64 B BVH2 nodes (two child boxes + two child links), 64 B
+//     aligned so one node = one half L2 line; leaves index a Morton-ordered
+//     array of 48 B primitive records (3 x float4: world-space triangle
+//     vertices; the first w carries the global primitive id).
+//   * Shading data stays in object space and is gathered only on hits
+//     (reference: geometry.h:48-96 interpolates object-space attributes then
+//     transforms), so the traversal working set is nodes + prim records only.
+#pragma once
+
+#include "../../include/pupil_pt.h"
+#include "pt_math.h"
+
+namespace pupil {
+
+// cuda::Texture (framework/cuda/texture.h:10-57)
+struct DevTexture {
+    uint32_t type;  // PUPIL_TEX_*
+    uint32_t width, height;
+    uint32_t filter;  // bitmap: 0 point, 1 linear
+    float c0[3];
+    float c1[3];
+    float r0[4];  // transform row 0
+    float r1[4];  // transform row 1
+    const float4 *data;  // bitmap texels (device)
+};
+
+// Flattened optix::material::Material (render/material/optix_material.h:87-98)
+// with the host precompute of optix_material.cpp:87-119 already applied.
+struct DevMaterial {
+    uint32_t type;
+    uint32_t twosided;
+    uint32_t nonlinear;
+    float eta;                       // int_ior / ext_ior
+    float int_fdr;                   // plastic: DiffuseReflectance(1/eta)
+    float specular_sampling_weight;  // plastic
+    float pad[2];
+    DevTexture tex[4];
+};
+
+// optix::Emitter (render/emitter.h:13-24)
+struct DevEmitter {
+    uint32_t type;
+    float select_probability;
+    float area;
+    float radius;
+    DevTexture radiance;
+    vec3 pos[3];
+    vec3 nrm[3];
+    vec2 tex[3];
+    vec3 center;
+    vec3 color;
+    // env map
+    float scale;
+    float normalization;
+    uint32_t map_w, map_h;
+    float to_world[9];
+    float to_local[9];
+    const float *row_cdf;     // map_h + 1
+    const float *col_cdf;     // (map_w + 1) * map_h
+    const float *row_weight;  // map_h
+};
+
+struct DevInstance {
+    float to_world[12];
+    float to_object[12];
+    uint32_t kind;  // PUPIL_SHAPE_*
+    uint32_t material;
+    uint32_t prim_offset;  // first global primitive id
+    int32_t emitter_offset;
+    uint32_t flip_normals;
+    uint32_t flip_tex_coords;
+    // object-space mesh attributes (null for spheres / missing)
+    const float *positions;
+    const float *normals;
+    const float *texcoords;
+    const uint32_t *indices;
+};
+
+struct alignas(16) BvhNode {
+    float4 lo0;  // xyz = child0 min, w = child0 link (int bits)
+    float4 hi0;  // xyz = child0 max, w = child1 link
+    float4 lo1;  // xyz = child1 min
+    float4 hi1;  // xyz = child1 max
+};
+
+// Child link encoding: link >= 0 -> internal node index; link < 0 -> leaf,
+// ~link = (first_prim << 3) | (count - 1), count in [1, 8].
+constexpr int kLeafMax = 8;
+PT_HD int make_leaf(uint32_t first, uint32_t count) { return ~(int)((first << 3) | (count - 1)); }
+PT_HD uint32_t leaf_first(int link) { return ((uint32_t)~link) >> 3; }
+PT_HD uint32_t leaf_count(int link) { return (((uint32_t)~link) & 7u) + 1u; }
+
+constexpr uint32_t kPrimSphereBit = 0x80000000u;
+
+struct Camera {
+    float s2c[16];  // sample_to_camera, row-major (mat4x4 r0..r3)
+    float c2w[16];  // camera_to_world
+};
+
+struct DeviceScene {
+    const BvhNode *nodes;
+    const float4 *prims;  // 3 float4 per primitive, Morton order
+    uint32_t num_prims;
+    uint32_t root_link;   // link of the root (internal 0 or a leaf)
+    const uint32_t *prim_inst;  // global prim id -> instance
+    const DevInstance *instances;
+    const DevMaterial *materials;
+    const DevEmitter *areas;
+    const float *area_cdf;  // sequential CDF of select_probability (emitter.h:110-120)
+    uint32_t num_areas;
+    uint32_t has_env;
+    const DevEmitter *env;
+    Camera camera;
+};
+
+}  // namespace pupil

@@ -1,0 +1,219 @@
+"""Benchmark / parity scenes (BASELINE.json configs).
+
+* ``cornell_xml``       config 1: the reference's Cornell box (data/static/
+  cornellbox.xml geometry: 6 rectangles + 2 cubes, light radiance (17,12,4)),
+  written as mitsuba XML so the C++ XML loader is exercised.
+* ``cornell_materials`` config 2: the Cornell box with ShortBox / TallBox and
+  added spheres carrying the seven reference BSDF types (parameters of
+  data/static/material_test.xml).
+* ``sphere_field``      configs 3/4: procedural field of tessellated spheres
+  (2,000 triangles each) over a floor, one rectangle area light.
+* ``instanced_field``   config 5 geometry (instances of one sphere-field BLAS).
+
+Geometry is generated with numpy's PCG64 from a fixed seed, so every rank of
+a multi-GPU run builds the identical scene.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from . import world as W
+
+# data/static/cornellbox.xml transforms (row-major to_world of each shape)
+CORNELL_SHAPES = [
+    ("rectangle", "Floor", "0.725, 0.71, 0.68",
+     "-4.37114e-008 1 4.37114e-008 0 0 -8.74228e-008 2 0 1 4.37114e-008 1.91069e-015 0 0 0 0 1"),
+    ("rectangle", "Ceiling", "0.725, 0.71, 0.68",
+     "-1 7.64274e-015 -1.74846e-007 0 8.74228e-008 8.74228e-008 -2 2 0 -1 -4.37114e-008 0 0 0 0 1"),
+    ("rectangle", "BackWall", "0.725, 0.71, 0.68",
+     "1.91069e-015 1 1.31134e-007 0 1 3.82137e-015 -8.74228e-008 1 -4.37114e-008 1.31134e-007 -2 -1 0 0 0 1"),
+    ("rectangle", "RightWall", "0.14, 0.45, 0.091",
+     "4.37114e-008 -1.74846e-007 2 1 1 3.82137e-015 -8.74228e-008 1 3.82137e-015 1 2.18557e-007 0 0 0 0 1"),
+    ("rectangle", "LeftWall", "0.63, 0.065, 0.05",
+     "-4.37114e-008 8.74228e-008 -2 -1 1 3.82137e-015 -8.74228e-008 1 0 -1 -4.37114e-008 0 0 0 0 1"),
+    ("cube", "ShortBox", "0.725, 0.71, 0.68",
+     "0.0851643 0.289542 1.31134e-008 0.328631 3.72265e-009 1.26563e-008 -0.3 0.3 -0.284951 0.0865363 "
+     "5.73206e-016 0.374592 0 0 0 1"),
+    ("cube", "TallBox", "0.725, 0.71, 0.68",
+     "0.286776 0.098229 -2.29282e-015 -0.335439 -4.36233e-009 1.23382e-008 -0.6 0.6 -0.0997984 0.282266 "
+     "2.62268e-008 -0.291415 0 0 0 1"),
+]
+CORNELL_LIGHT = ("0.235 -1.66103e-008 -7.80685e-009 -0.005 -2.05444e-008 3.90343e-009 -0.0893 1.98 "
+                 "2.05444e-008 0.19 8.30516e-009 -0.03 0 0 0 1")
+CORNELL_SENSOR = "-1 0 0 0 0 1 0 1 0 0 -1 6.8 0 0 0 1"
+
+
+def cornell_xml(path: str, width=256, height=256, max_depth=4, bsdf_overrides=None, extra_shapes="") -> str:
+    """Write the Cornell box scene (config 1) as mitsuba-3 XML and return its path.
+
+    ``bsdf_overrides`` maps a shape id to an XML <bsdf> snippet (config 2)."""
+    bsdf_overrides = bsdf_overrides or {}
+    lines = [
+        '<scene version="3.0.0">',
+        f'  <default name="resx" value="{width}"/>',
+        f'  <default name="resy" value="{height}"/>',
+        f'  <default name="max_depth" value="{max_depth}"/>',
+        '  <integrator type="path"><integer name="max_depth" value="$max_depth"/></integrator>',
+        '  <sensor type="perspective">',
+        '    <float name="fov" value="19.5"/>',
+        f'    <transform name="to_world"><matrix value="{CORNELL_SENSOR}"/></transform>',
+        '    <sampler type="independent"><integer name="sample_count" value="64"/></sampler>',
+        '    <film type="hdrfilm"><integer name="width" value="$resx"/>'
+        '<integer name="height" value="$resy"/><rfilter type="tent"/></film>',
+        '  </sensor>',
+    ]
+    for kind, sid, refl, mat in CORNELL_SHAPES:
+        bsdf = bsdf_overrides.get(sid) or (
+            f'<bsdf type="twosided" id="{sid}BSDF"><bsdf type="diffuse">'
+            f'<rgb name="reflectance" value="{refl}"/></bsdf></bsdf>')
+        lines += [f'  <shape type="{kind}" id="{sid}">',
+                  f'    <transform name="to_world"><matrix value="{mat}"/></transform>',
+                  f'    {bsdf}', '  </shape>']
+    lines += ['  <bsdf type="twosided" id="LightBSDF"><bsdf type="diffuse">'
+              '<rgb name="reflectance" value="0, 0, 0"/></bsdf></bsdf>',
+              '  <shape type="rectangle" id="Light">',
+              f'    <transform name="to_world"><matrix value="{CORNELL_LIGHT}"/></transform>',
+              '    <ref id="LightBSDF"/>',
+              '    <emitter type="area"><rgb name="radiance" value="17, 12, 4"/></emitter>',
+              '  </shape>', extra_shapes, '</scene>']
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        f.write("\n".join(lines))
+    return path
+
+
+# material_test.xml parameters (data/static/material_test.xml:30-114)
+MATERIAL_BSDFS = {
+    "dielectric": '<bsdf type="dielectric"><float name="int_ior" value="1.5"/>'
+                  '<float name="ext_ior" value="1"/></bsdf>',
+    "roughdielectric": '<bsdf type="roughdielectric"><float name="alpha" value="0.35"/>'
+                       '<float name="int_ior" value="1.5"/><float name="ext_ior" value="1"/></bsdf>',
+    "conductor": '<bsdf type="conductor"><rgb name="specular_reflectance" value="0.3, 0.3, 0.3"/>'
+                 '<rgb name="eta" value="0.200438, 0.924033, 1.10221"/>'
+                 '<rgb name="k" value="3.91295, 2.45285, 2.14219"/></bsdf>',
+    "roughconductor": '<bsdf type="roughconductor"><float name="alpha" value="0.35"/>'
+                      '<rgb name="specular_reflectance" value="0.3, 0.3, 0.3"/>'
+                      '<rgb name="eta" value="0.200438, 0.924033, 1.10221"/>'
+                      '<rgb name="k" value="3.91295, 2.45285, 2.14219"/></bsdf>',
+    "plastic": '<bsdf type="plastic"><float name="int_ior" value="1.5"/><float name="ext_ior" value="1"/>'
+               '<boolean name="nonlinear" value="false"/>'
+               '<rgb name="diffuse_reflectance" value="0.647814, 0.647814, 0.647814"/></bsdf>',
+    "roughplastic": '<bsdf type="roughplastic"><float name="alpha" value="0.35"/>'
+                    '<float name="int_ior" value="1.5"/><float name="ext_ior" value="1"/>'
+                    '<boolean name="nonlinear" value="false"/>'
+                    '<rgb name="diffuse_reflectance" value="0.647814, 0.647814, 0.647814"/></bsdf>',
+}
+
+
+def cornell_materials_xml(path: str, width=1024, height=1024, max_depth=6) -> str:
+    """Config 2: Cornell box whose boxes and five added spheres carry all seven BSDFs."""
+    overrides = {"ShortBox": MATERIAL_BSDFS["roughconductor"], "TallBox": MATERIAL_BSDFS["plastic"]}
+    spheres = []
+    placements = [("dielectric", (-0.55, 0.25, 0.45), 0.22), ("roughdielectric", (0.0, 0.18, 0.62), 0.17),
+                  ("conductor", (0.55, 0.78, 0.2), 0.17), ("roughplastic", (-0.3, 1.45, -0.4), 0.2),
+                  ("roughconductor", (0.45, 1.55, -0.5), 0.15)]
+    for i, (name, c, r) in enumerate(placements):
+        spheres.append(f'  <shape type="sphere" id="sphere{i}"><point name="center" value="{c[0]}, {c[1]}, {c[2]}"/>'
+                       f'<float name="radius" value="{r}"/>{MATERIAL_BSDFS[name]}</shape>')
+    return cornell_xml(path, width, height, max_depth, overrides, "\n".join(spheres))
+
+
+def uv_sphere(slices=40, stacks=26):
+    """Tessellated unit sphere with 2*slices*(stacks-1) triangles (2,000 by default)."""
+    verts, norms, uvs = [], [], []
+    for i in range(stacks + 1):
+        th = np.pi * i / stacks
+        for j in range(slices + 1):
+            ph = 2 * np.pi * j / slices
+            p = (np.sin(th) * np.cos(ph), np.cos(th), np.sin(th) * np.sin(ph))
+            verts.append(p)
+            norms.append(p)
+            uvs.append((j / slices, i / stacks))
+    idx = []
+    row = slices + 1
+    for i in range(stacks):
+        for j in range(slices):
+            a, b = i * row + j, i * row + j + 1
+            c, d = (i + 1) * row + j, (i + 1) * row + j + 1
+            if i != 0:
+                idx.append((a, c, b))
+            if i != stacks - 1:
+                idx.append((b, c, d))
+    return (np.asarray(verts, np.float32), np.asarray(norms, np.float32), np.asarray(uvs, np.float32),
+            np.asarray(idx, np.uint32))
+
+
+def _field_geometry(num_spheres: int, seed: int, box=10.0):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    # jittered grid keeps spheres non-overlapping at any count
+    n = int(np.ceil(num_spheres ** (1.0 / 3.0)))
+    cell = box / n
+    cells = rng.permutation(n ** 3)[:num_spheres]
+    centers, radii, albedo = [], [], []
+    for c in cells:
+        ix, iy, iz = c % n, (c // n) % n, c // (n * n)
+        r = cell * rng.uniform(0.2, 0.4)
+        jitter = (cell / 2 - r) * rng.uniform(-1, 1, 3)
+        centers.append((np.array([ix, iy, iz]) + 0.5) * cell - box / 2 + jitter + np.array([0, box / 2, 0]))
+        radii.append(r)
+        albedo.append(rng.uniform(0.3, 0.8, 3))
+    return np.asarray(centers), np.asarray(radii), np.asarray(albedo)
+
+
+def sphere_field(num_spheres=500, width=1920, height=1080, max_depth=4, seed=1, slices=40, stacks=26,
+                 merge=True) -> W.World:
+    """Configs 3/4: ``num_spheres`` x 2,000-triangle spheres (+2 floor, +2 light triangles).
+
+    With ``merge`` the spheres are baked into one world-space mesh (one
+    instance, like a single OBJ); otherwise one instance per sphere."""
+    wd = W.World()
+    wd.set_film(width, height, max_depth)
+    box = 10.0
+    centers, radii, albedo = _field_geometry(num_spheres, seed, box)
+    v, nrm, uv, idx = uv_sphere(slices, stacks)
+    if merge:
+        P, N, T, I = [], [], [], []
+        base = 0
+        mats = []
+        for c, r in zip(centers, radii):
+            P.append(v * r + c)
+            N.append(nrm)
+            T.append(uv)
+            I.append(idx + base)
+            base += len(v)
+        # one material per sphere needs one instance per sphere; the merged
+        # variant groups spheres into 8 albedo classes, one mesh each
+        groups = np.arange(num_spheres) % 8
+        for g in range(8):
+            sel = np.nonzero(groups == g)[0]
+            if sel.size == 0:
+                continue
+            pos = np.concatenate([P[k] for k in sel])
+            nn = np.concatenate([N[k] for k in sel])
+            tt = np.concatenate([T[k] for k in sel])
+            off = np.cumsum([0] + [len(P[k]) for k in sel[:-1]])
+            ii = np.concatenate([idx + o for o in off])
+            s = wd.add_mesh(pos, ii, nn, tt)
+            m = wd.add_material(W.diffuse(tuple(albedo[sel[0]])))
+            wd.add_instance(s, m)
+            mats.append(m)
+    else:
+        s = wd.add_mesh(v, idx, nrm, uv)
+        for c, r, a in zip(centers, radii, albedo):
+            m = wd.add_material(W.diffuse(tuple(a)))
+            wd.add_instance(s, m, W.transform(scale=(r, r, r), translate=tuple(c)))
+    rect = wd.add_builtin("rectangle")
+    floor_m = wd.add_material(W.diffuse((0.6, 0.6, 0.6)))
+    wd.add_instance(rect, floor_m, W.transform(scale=(30, 30, 1), rotate=((1, 0, 0), -90), translate=(0, 0, 0)))
+    light_m = wd.add_material(W.twosided(W.diffuse((0.0, 0.0, 0.0))))
+    wd.add_instance(rect, light_m, W.transform(scale=(3, 3, 1), rotate=((1, 0, 0), 90), translate=(0, 14, 0)),
+                    emitter_radiance=(40.0, 38.0, 34.0))
+    cam = W.look_at_mitsuba((0.0, 9.0, 19.0), (0.0, 4.5, 0.0), (0, 1, 0))
+    wd.set_sensor(45.0, cam, fov_axis="y")
+    return wd
+
+
+def triangle_count(num_spheres, slices=40, stacks=26):
+    return num_spheres * 2 * slices * (stacks - 1) + 4
