@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--max-depth", type=int, default=4)
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1 only)")
-    ap.add_argument("--cpu-sample-stride", type=int, default=16, help="CPU baseline renders every k-th pixel")
+    ap.add_argument("--cpu-sample-stride", type=int, default=1, help="CPU baseline renders every k-th pixel")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--save", default="", help="write the frame as PNG (rank 0)")
     return ap.parse_args()
@@ -81,33 +81,18 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     # gather plumbing (rank 0 assembles the frame)
+    gather = None
     if world > 1:
-        counts = [0] * world
-        maps = []
-        for r in range(world):
-            import ctypes as C
+        from pupiloptixlab_amd.dist import FrameGather
 
-            n = C.c_uint32(0)
-            pt._lib.pupil_pt_local_pixels(args.width, args.height, args.tile, r, world, None, C.byref(n))
-            counts[r] = n.value
-            arr = np.zeros(n.value, np.uint32)
-            pt._lib.pupil_pt_local_pixels(args.width, args.height, args.tile, r, world,
-                                          arr.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(n))
-            maps.append(torch.from_numpy(arr.astype(np.int64)).to(dev))
-        max_local = max(counts)
-        send = torch.zeros((max_local, 4), dtype=torch.float32, device=dev)
-        recv = [torch.zeros_like(send) for _ in range(world)] if rank == 0 else None
-        full = torch.zeros((args.width * args.height, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+        gather = FrameGather(args.width, args.height, args.tile, rank, world, dev)
+        assert gather.n_local == n_local
 
     def frame():
         pt.mark_dirty()  # each step is a fresh 8-spp frame from seed 0
         pt.render(args.spp, stream=stream)
-        if world > 1:
-            send[:n_local].copy_(pt.buffers.get(FINAL_RESULT))
-            dist.gather(send, recv, dst=0)
-            if rank == 0:
-                for r in range(world):
-                    full.index_copy_(0, maps[r], recv[r][: counts[r]])
+        if gather is not None:
+            gather.gather(pt.buffers.get(FINAL_RESULT))
 
     # one instrumented frame for the traversal byte counts (untimed)
     pt.mark_dirty()
@@ -165,7 +150,7 @@ def main():
         if args.save:
             from tools import imgio
 
-            img = (full if world > 1 else pt.buffers.get(FINAL_RESULT)).cpu().numpy()
+            img = (gather.full if gather is not None else pt.buffers.get(FINAL_RESULT)).cpu().numpy()
             imgio.save_render(args.save, img.reshape(args.height, args.width, 4))
         out = {
             "metric": "Mrays/sec + ms/frame, 1M-tri scene @1920x1080 8spp; 1/2/4/8-GPU scaling",

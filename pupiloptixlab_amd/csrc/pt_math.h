@@ -73,7 +73,7 @@ PT_HD vec4 normalize(vec4 v) {
     return v4(v.x * inv_len, v.y * inv_len, v.z * inv_len, v.w * inv_len);
 }
 PT_HD vec3 lerp(vec3 a, vec3 b, float t) { return a + t * (b - a); }
-PT_HD float fabs_(float v) { return v < 0.f ? -v : v; }
+PT_HD float fabs_(float v) { return __builtin_fabsf(v); }  // IEEE abs (clears the sign of -0 too)
 PT_HD float fmax_(float a, float b) { return a > b ? a : b; }
 PT_HD float fmin_(float a, float b) { return a < b ? a : b; }
 

@@ -1,0 +1,55 @@
+"""Multi-GPU image-tile sharding (one process per GPU, torch.distributed).
+
+The reference is single-GPU; each pixel's path depends only on
+(pixel_index, random_seed) and the read-only scene (main.cu:40,53), so the
+frame shards into independent tiles with the BVH replicated on every GPU.
+Tile t (32x32, row-major) belongs to rank t % world (pupil_pt_local_pixels).
+Once per frame every rank's compact tile radiance is gathered to rank 0 over
+RCCL (backend "nccl") and scattered into the full image — one collective,
+~4 MB per rank at 1080p/8 GPUs.  Results are bit-identical to one GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .abi import check, load_library
+
+
+def local_pixels(width, height, tile, rank, world) -> np.ndarray:
+    lib = load_library()
+    n = C.c_uint32(0)
+    check(lib.pupil_pt_local_pixels(width, height, tile, rank, world, None, C.byref(n)))
+    out = np.zeros(max(1, n.value), np.uint32)
+    check(lib.pupil_pt_local_pixels(width, height, tile, rank, world, out.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                    C.byref(n)))
+    return out[: n.value]
+
+
+class FrameGather:
+    """Gathers every rank's compact (n_local, C) tile buffer into rank 0's full image."""
+
+    def __init__(self, width, height, tile, rank, world, device, channels=4):
+        import torch
+
+        self.rank, self.world = rank, world
+        self.maps = [torch.from_numpy(local_pixels(width, height, tile, r, world).astype(np.int64)).to(device)
+                     for r in range(world)]
+        self.counts = [len(m) for m in self.maps]
+        self.n_local = self.counts[rank]
+        self.send = torch.zeros((max(self.counts), channels), dtype=torch.float32, device=device)
+        self.recv = [torch.zeros_like(self.send) for _ in range(world)] if rank == 0 else None
+        self.full = (torch.zeros((width * height, channels), dtype=torch.float32, device=device)
+                     if rank == 0 else None)
+
+    def gather(self, local):
+        import torch.distributed as dist
+
+        self.send[: self.n_local].copy_(local)
+        dist.gather(self.send, self.recv, dst=0)
+        if self.rank == 0:
+            for r in range(self.world):
+                self.full.index_copy_(0, self.maps[r], self.recv[r][: self.counts[r]])
+            return self.full
+        return None

@@ -204,16 +204,25 @@ def sphere_field(num_spheres=500, width=1920, height=1080, max_depth=4, seed=1, 
         for c, r, a in zip(centers, radii, albedo):
             m = wd.add_material(W.diffuse(tuple(a)))
             wd.add_instance(s, m, W.transform(scale=(r, r, r), translate=tuple(c)))
+    # closed room around the field (floor, ceiling, four walls: 12 triangles)
+    # so every camera and bounce ray hits geometry, like an interior scene
     rect = wd.add_builtin("rectangle")
-    floor_m = wd.add_material(W.diffuse((0.6, 0.6, 0.6)))
-    wd.add_instance(rect, floor_m, W.transform(scale=(30, 30, 1), rotate=((1, 0, 0), -90), translate=(0, 0, 0)))
+    wall_m = wd.add_material(W.twosided(W.diffuse((0.6, 0.6, 0.6))))
+    room = [((8, 12, 1), ((1, 0, 0), -90), (0, 0, 2)),     # floor      y = 0
+            ((8, 12, 1), ((1, 0, 0), 90), (0, 14, 2)),     # ceiling    y = 14
+            ((8, 7, 1), None, (0, 7, -10)),                # back wall  z = -10
+            ((8, 7, 1), ((0, 1, 0), 180), (0, 7, 14)),     # front wall z = 14
+            ((12, 7, 1), ((0, 1, 0), 90), (-8, 7, 2)),     # left wall  x = -8
+            ((12, 7, 1), ((0, 1, 0), -90), (8, 7, 2))]     # right wall x = 8
+    for sc, rot, tr in room:
+        wd.add_instance(rect, wall_m, W.transform(scale=sc, rotate=rot, translate=tr))
     light_m = wd.add_material(W.twosided(W.diffuse((0.0, 0.0, 0.0))))
-    wd.add_instance(rect, light_m, W.transform(scale=(3, 3, 1), rotate=((1, 0, 0), 90), translate=(0, 14, 0)),
+    wd.add_instance(rect, light_m, W.transform(scale=(3, 3, 1), rotate=((1, 0, 0), 90), translate=(0, 13.9, 0)),
                     emitter_radiance=(40.0, 38.0, 34.0))
-    cam = W.look_at_mitsuba((0.0, 9.0, 19.0), (0.0, 4.5, 0.0), (0, 1, 0))
-    wd.set_sensor(45.0, cam, fov_axis="y")
+    cam = W.look_at_mitsuba((0.0, 6.0, 13.0), (0.0, 4.6, 0.0), (0, 1, 0))
+    wd.set_sensor(50.0, cam, fov_axis="y")
     return wd
 
 
 def triangle_count(num_spheres, slices=40, stacks=26):
-    return num_spheres * 2 * slices * (stacks - 1) + 4
+    return num_spheres * 2 * slices * (stacks - 1) + 14

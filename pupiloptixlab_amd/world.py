@@ -199,6 +199,7 @@ class World:
         """Flattened scene (pointers owned by the world; valid until it changes)."""
         d = abi.SceneDesc()
         check(self._lib.pupil_world_get_desc(self._h, C.byref(d)))
+        d._owner = self  # the arrays live in this world: keep it alive with the desc
         self._desc = d
         return d
 
