@@ -322,6 +322,119 @@ __global__ void k_emit(int n, const uint32_t *sorted_vals, const Aabb *prim_boxe
     nodes[i] = nd;
 }
 
+// ---------------------------------------------------------------- BVH4 collapse
+// Binary nodes at even depth become 4-wide nodes whose children are their
+// grandchildren (or the child itself where the child is a leaf).
+__global__ void k_depth(int n, const int *parent_internal, uint32_t *depth) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1) return;
+    uint32_t d = 0;
+    for (int p = i; p != 0; p = parent_internal[p]) d++;
+    depth[i] = d;
+}
+
+__global__ void k_flag4(int n, const int2 *ranges, const uint32_t *depth, uint32_t leaf_size, uint32_t *flags) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1) return;
+    const int2 r = ranges[i];
+    flags[i] = ((depth[i] & 1u) == 0u && (uint32_t)(r.y - r.x + 1) > leaf_size) ? 1u : 0u;
+}
+
+// decode used by the traversal: origin + (float)q * scale (q*scale is exact)
+__device__ __forceinline__ float qdecode(float origin, uint32_t q, float scale) { return origin + (float)q * scale; }
+
+// Conservative 8-bit quantisation of up to 4 child intervals on one axis.
+__device__ void quantize_axis(float lo, float hi, const float *clo, const float *chi, int nk, float &origin,
+                              uint32_t &ebyte, uint32_t &qlo, uint32_t &qhi) {
+    origin = lo;
+    const float ext = hi - lo;
+    float scale;
+    if (!(ext > 0.f)) {
+        scale = __uint_as_float(1u << 23);  // 2^-126
+    } else {
+        scale = exp2f(ceilf(log2f(ext / 254.f)));
+        if (!(scale > 0.f)) scale = __uint_as_float(1u << 23);
+    }
+    for (int attempt = 0; attempt < 8; attempt++) {
+        bool ok = true;
+        qlo = 0u;
+        qhi = 0u;
+        for (int k = 0; k < 4; k++) {
+            uint32_t a = 255u, b = 0u;  // empty slot: lo > hi
+            if (k < nk) {
+                float fa = floorf((clo[k] - origin) / scale);
+                float fb = ceilf((chi[k] - origin) / scale);
+                fa = fminf(fmaxf(fa, 0.f), 255.f);
+                fb = fminf(fmaxf(fb, 0.f), 255.f);
+                a = (uint32_t)fa;
+                b = (uint32_t)fb;
+                while (a > 0u && qdecode(origin, a, scale) > clo[k]) a--;
+                while (b < 255u && qdecode(origin, b, scale) < chi[k]) b++;
+                if (qdecode(origin, a, scale) > clo[k] || qdecode(origin, b, scale) < chi[k]) ok = false;
+            }
+            qlo |= a << (8 * k);
+            qhi |= b << (8 * k);
+        }
+        if (ok) break;
+        scale = scale * 2.f;
+    }
+    ebyte = (__float_as_uint(scale) >> 23) & 0xFFu;
+}
+
+__global__ void k_emit4(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
+                        const int2 *ranges, const Aabb *node_boxes, const uint32_t *flags, const uint32_t *idx4,
+                        uint32_t leaf_size, Bvh4Node *nodes4) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1 || !flags[i]) return;
+    int link[4];
+    Aabb box[4];
+    int nk = 0;
+    auto add = [&](int c) {
+        if (c < 0) {
+            link[nk] = make_leaf((uint32_t)~c, 1u);
+            box[nk] = prim_boxes[sorted_vals[~c]];
+        } else {
+            const int2 r = ranges[c];
+            const uint32_t cnt = (uint32_t)(r.y - r.x + 1);
+            link[nk] = cnt <= leaf_size ? make_leaf((uint32_t)r.x, cnt) : (int)idx4[c];
+            box[nk] = node_boxes[c];
+        }
+        nk++;
+    };
+    const int2 c = children[i];
+    for (int s = 0; s < 2; s++) {
+        const int ch = s == 0 ? c.x : c.y;
+        bool expand = false;
+        if (ch >= 0) {
+            const int2 r = ranges[ch];
+            expand = (uint32_t)(r.y - r.x + 1) > leaf_size;  // odd-depth internal node: absorb it
+        }
+        if (expand) {
+            const int2 g = children[ch];
+            add(g.x);
+            add(g.y);
+        } else {
+            add(ch);
+        }
+    }
+    const Aabb nb = node_boxes[i];
+    float clo[3][4], chi[3][4];
+    for (int k = 0; k < 4; k++)
+        for (int a = 0; a < 3; a++) {
+            clo[a][k] = k < nk ? box[k].lo[a] : 0.f;
+            chi[a][k] = k < nk ? box[k].hi[a] : 0.f;
+        }
+    Bvh4Node o;
+    uint32_t ex, ey, ez;
+    quantize_axis(nb.lo[0], nb.hi[0], clo[0], chi[0], nk, o.ox, ex, o.qlo_x, o.qhi_x);
+    quantize_axis(nb.lo[1], nb.hi[1], clo[1], chi[1], nk, o.oy, ey, o.qlo_y, o.qhi_y);
+    quantize_axis(nb.lo[2], nb.hi[2], clo[2], chi[2], nk, o.oz, ez, o.qlo_z, o.qhi_z);
+    o.exps = ex | (ey << 8) | (ez << 16);
+    for (int k = 0; k < 4; k++) o.child[k] = k < nk ? link[k] : kEmptyLink;
+    o.pad[0] = o.pad[1] = 0u;
+    nodes4[idx4[i]] = o;
+}
+
 __global__ void k_reorder(int n, const uint32_t *sorted_vals, const float4 *recs_in, float4 *recs_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -340,8 +453,10 @@ hipError_t dmalloc(T **p, size_t count) {
 
 void free_lbvh(BvhBuildOutput &out) {
     if (out.nodes) (void)hipFree(out.nodes);
+    if (out.nodes4) (void)hipFree(out.nodes4);
     if (out.prims) (void)hipFree(out.prims);
     out.nodes = nullptr;
+    out.nodes4 = nullptr;
     out.prims = nullptr;
 }
 
@@ -408,11 +523,35 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
                                parent_leaf, node_boxes, flags);
             hipLaunchKernelGGL(k_emit, dim3(gi), dim3(kBlock), 0, s, n, vi, boxes, children, ranges, node_boxes,
                                leaf_size, out.nodes);
+            // 4-wide quantized tree: depth parity -> flags -> compact indices -> nodes
+            uint32_t *depth = ko, *flags4 = vo, *idx4 = nullptr;  // the sort's free ping-pong buffers
+            err = dmalloc(&idx4, n);
+            hipLaunchKernelGGL(k_depth, dim3(gi), dim3(kBlock), 0, s, n, parent_internal, depth);
+            hipLaunchKernelGGL(k_flag4, dim3(gi), dim3(kBlock), 0, s, n, ranges, depth, leaf_size, flags4);
+            uint32_t tail[2] = {0, 0};
+            if (!err) {
+                (void)hipMemcpyAsync(idx4, flags4, sizeof(uint32_t) * (n - 1), hipMemcpyDeviceToDevice, s);
+                hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, idx4, (uint32_t)(n - 1));
+                (void)hipMemcpyAsync(&tail[0], idx4 + (n - 2), sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+                (void)hipMemcpyAsync(&tail[1], flags4 + (n - 2), sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+                (void)hipStreamSynchronize(s);
+                out.num_nodes4 = tail[0] + tail[1];
+                err = dmalloc(&out.nodes4, out.num_nodes4 ? out.num_nodes4 : 1);
+            }
+            if (!err)
+                hipLaunchKernelGGL(k_emit4, dim3(gi), dim3(kBlock), 0, s, n, vi, boxes, children, ranges, node_boxes,
+                                   flags4, idx4, leaf_size, out.nodes4);
+            (void)hipStreamSynchronize(s);
+            if (idx4) (void)hipFree(idx4);
+        } else {
+            err = dmalloc(&out.nodes4, 1);
+            out.num_nodes4 = 0;
         }
         hipLaunchKernelGGL(k_reorder, dim3(g), dim3(kBlock), 0, s, n, vi, recs, out.prims);
         out.num_nodes = n > 1 ? (uint32_t)(n - 1) : 0u;
         out.root_link = ((uint32_t)n <= leaf_size) ? (uint32_t)make_leaf(0u, (uint32_t)n) : 0u;
-        err = hipGetLastError();
+        out.root_link4 = out.root_link;
+        if (!err) err = hipGetLastError();
     }
     (void)hipEventRecord(e1, s);
     (void)hipEventSynchronize(e1);

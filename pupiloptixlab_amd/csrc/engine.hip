@@ -10,6 +10,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -428,6 +429,11 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     sc.prims = pt->bvh.prims;
     sc.num_prims = pt->num_prims;
     sc.root_link = pt->bvh.root_link;
+    sc.nodes4 = pt->bvh.nodes4;
+    sc.root_link4 = pt->bvh.root_link4;
+    sc.bvh_width = 4;
+    if (const char *w = std::getenv("PUPIL_BVH_WIDTH"))  // A/B switch for the node format
+        if (std::atoi(w) == 2) sc.bvh_width = 2;
     sc.prim_inst = d_prim_inst;
     sc.instances = d_insts;
     sc.materials = d_mats;
@@ -445,7 +451,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
-    pt->totals.bvh_nodes = pt->bvh.num_nodes;
+    pt->totals.bvh_nodes = pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes;
     pt->totals.bvh_prims = pt->num_prims;
     pt->totals.build_ms = pt->build_ms;
     *out = pt;

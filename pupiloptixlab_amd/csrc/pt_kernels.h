@@ -10,7 +10,7 @@ namespace pupil {
 
 constexpr int kTraceBlock = 128;
 constexpr int kStackLds = 32;   // per-thread LDS stack entries
-constexpr int kStackOvf = 64;   // per-thread global overflow entries
+constexpr int kStackOvf = 96;   // per-thread global overflow entries
 constexpr int kShadeBlock = 256;
 constexpr uint32_t kNumQueues = 9;  // 0 = miss, 1..7 = EMatType, 8 = unknown material
 constexpr uint32_t kMissIndex = 0xFFFFFFFFu;
@@ -83,9 +83,12 @@ struct BvhBuildInput {
 };
 struct BvhBuildOutput {
     BvhNode *nodes;     // device, max(1, n-1)
+    Bvh4Node *nodes4;   // device, collapsed 4-wide quantized tree
     float4 *prims;      // device, 3 * n
     uint32_t root_link;
+    uint32_t root_link4;
     uint32_t num_nodes;
+    uint32_t num_nodes4;
 };
 int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms);
 void free_lbvh(BvhBuildOutput &out);

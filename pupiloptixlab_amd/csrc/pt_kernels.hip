@@ -46,11 +46,15 @@ struct Stack {
     int *lds;          // this thread's column base
     int *ovf;          // this thread's overflow base
     uint32_t ovf_stride;
+    // indices are clamped to the capacity: a pathological tree can only give
+    // a wrong answer, never an out-of-bounds access
     __device__ __forceinline__ void store(int i, int v) {
+        i = min(i, kStackLds + kStackOvf - 1);
         if (i < kStackLds) lds[i * kTraceBlock] = v;
         else ovf[(size_t)(i - kStackLds) * ovf_stride] = v;
     }
     __device__ __forceinline__ int load(int i) const {
+        i = max(0, min(i, kStackLds + kStackOvf - 1));
         return i < kStackLds ? lds[i * kTraceBlock] : ovf[(size_t)(i - kStackLds) * ovf_stride];
     }
 };
@@ -148,6 +152,135 @@ __device__ __forceinline__ bool traverse(const DeviceScene &sc, const RayPre &r,
     return found;
 }
 
+// Leaf intersection shared by both node formats.
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool intersect_leaf(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
+                                               float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
+                                               float &bb2, uint32_t &prims_tested, bool &found) {
+    const uint32_t first = leaf_first(leaf);
+    const uint32_t count = leaf_count(leaf);
+    for (uint32_t i = first; i < first + count; i++) {
+        const float4 a = sc.prims[3 * i + 0];
+        const float4 b = sc.prims[3 * i + 1];
+        const uint32_t ref = __float_as_uint(a.w);
+        const uint32_t key = ref & ~kPrimSphereBit;
+        if (STATS) prims_tested++;
+        float t, b1 = 0.f, b2 = 0.f;
+        bool hit;
+        if (ref & kPrimSphereBit) {
+            const DevInstance &in = sc.instances[__float_as_uint(b.w)];
+            hit = intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, t);
+        } else {
+            const float4 c = sc.prims[3 * i + 2];
+            hit = intersect_triangle(r, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), tmin, tmax, t, b1,
+                                     b2);
+        }
+        if (hit) {
+            if (ANY) {
+                found = true;
+                return true;
+            }
+            if (t < tmax || key < best_key) {
+                tmax = t;
+                best_key = key;
+                best_idx = i;
+                bb1 = b1;
+                bb2 = b2;
+                found = true;
+            }
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ void cswap(float &ta, int &la, float &tb, int &lb) {
+    if (tb < ta) {
+        const float t = ta;
+        ta = tb;
+        tb = t;
+        const int l = la;
+        la = lb;
+        lb = l;
+    }
+}
+
+// 4-wide quantized traversal (same while-while / postponed-leaf structure).
+// Child boxes are decoded exactly as the builder verified them, then slab-
+// tested with the conservative test; hits are sorted near-to-far with a
+// 5-comparator network, the nearest is descended, the rest pushed.
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool traverse4(const DeviceScene &sc, const RayPre &r, float tmin, float &tmax,
+                                          uint32_t &best_key, uint32_t &best_idx, float &bb1, float &bb2, Stack &st,
+                                          uint32_t &nodes_visited, uint32_t &prims_tested) {
+    constexpr float kInf = __builtin_huge_valf();
+    int sp = 0;
+    st.store(0, kSentinel);
+    int node = (int)sc.root_link4;
+    int leaf = 0;
+    bool found = false;
+    while (node != kSentinel) {
+        while ((uint32_t)node < (uint32_t)kSentinel) {
+            const Bvh4Node n = sc.nodes4[node];
+            if (STATS) nodes_visited++;
+            const float sx = __uint_as_float((n.exps & 0xFFu) << 23);
+            const float sy = __uint_as_float(((n.exps >> 8) & 0xFFu) << 23);
+            const float sz = __uint_as_float(((n.exps >> 16) & 0xFFu) << 23);
+            float t[4];
+            int l[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const vec3 lo = v3(n.ox + (float)((n.qlo_x >> (8 * k)) & 0xFFu) * sx,
+                                   n.oy + (float)((n.qlo_y >> (8 * k)) & 0xFFu) * sy,
+                                   n.oz + (float)((n.qlo_z >> (8 * k)) & 0xFFu) * sz);
+                const vec3 hi = v3(n.ox + (float)((n.qhi_x >> (8 * k)) & 0xFFu) * sx,
+                                   n.oy + (float)((n.qhi_y >> (8 * k)) & 0xFFu) * sy,
+                                   n.oz + (float)((n.qhi_z >> (8 * k)) & 0xFFu) * sz);
+                l[k] = n.child[k];
+                const float te = box_entry(r, lo, hi, tmin, tmax);
+                t[k] = l[k] != kEmptyLink ? te : kInf;
+            }
+            cswap(t[0], l[0], t[1], l[1]);
+            cswap(t[2], l[2], t[3], l[3]);
+            cswap(t[0], l[0], t[2], l[2]);
+            cswap(t[1], l[1], t[3], l[3]);
+            cswap(t[1], l[1], t[2], l[2]);
+            if (t[0] == kInf) {
+                node = st.load(sp);
+                sp--;
+            } else {
+                node = l[0];
+                if (t[3] != kInf) st.store(++sp, l[3]);
+                if (t[2] != kInf) st.store(++sp, l[2]);
+                if (t[1] != kInf) st.store(++sp, l[1]);
+            }
+            if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
+                leaf = node;
+                node = st.load(sp);
+                sp--;
+            }
+            if (!__any(leaf >= 0)) break;
+        }
+        while (leaf < 0) {
+            if (intersect_leaf<ANY, STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, bb1, bb2, prims_tested, found))
+                return true;
+            leaf = node;
+            if (node < 0) {
+                node = st.load(sp);
+                sp--;
+            }
+        }
+    }
+    return found;
+}
+
+template <bool ANY, bool STATS, int W>
+__device__ __forceinline__ bool trace_ray(const DeviceScene &sc, const RayPre &r, float tmin, float &tmax,
+                                          uint32_t &best_key, uint32_t &best_idx, float &bb1, float &bb2, Stack &st,
+                                          uint32_t &nv, uint32_t &pt) {
+    if constexpr (W == 4) return traverse4<ANY, STATS>(sc, r, tmin, tmax, best_key, best_idx, bb1, bb2, st, nv, pt);
+    else return traverse<ANY, STATS>(sc, r, tmin, tmax, best_key, best_idx, bb1, bb2, st, nv, pt);
+}
+
 template <bool STATS>
 __device__ __forceinline__ void flush_stats(const TraceStats *stats, uint32_t nv, uint32_t pt) {
     if (!STATS) return;
@@ -164,7 +297,7 @@ __device__ __forceinline__ void flush_stats(const TraceStats *stats, uint32_t nv
 }
 
 // ------------------------------------------------------------------ extend
-template <bool STATS>
+template <bool STATS, int W>
 __global__ __launch_bounds__(kTraceBlock) void k_extend(DeviceScene sc, PathState ps, Queues q,
                                                         const uint32_t *queue, const uint32_t *queue_count,
                                                         uint32_t static_count, int *ovf, uint32_t ovf_threads,
@@ -193,7 +326,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend(DeviceScene sc, PathStat
             float tmax = kMaxDistance;
             uint32_t best_key = 0xFFFFFFFFu, best_idx = kMissIndex;
             float b1 = 0.f, b2 = 0.f;
-            const bool hit = traverse<false, STATS>(sc, r, 0.001f, tmax, best_key, best_idx, b1, b2, st, nv, pt);
+            const bool hit = trace_ray<false, STATS, W>(sc, r, 0.001f, tmax, best_key, best_idx, b1, b2, st, nv, pt);
             ps.hit[p] = make_float4(hit ? tmax : -1.f, b1, b2, __uint_as_float(hit ? best_idx : kMissIndex));
             if (hit) {
                 const uint32_t mt = __float_as_uint(sc.prims[3 * best_idx + 2].w);
@@ -215,7 +348,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend(DeviceScene sc, PathStat
 }
 
 // ------------------------------------------------------------------ shadow
-template <bool STATS>
+template <bool STATS, int W>
 __global__ __launch_bounds__(kTraceBlock) void k_shadow(DeviceScene sc, PathState ps, Queues q, int *ovf,
                                                         uint32_t ovf_threads, TraceStats stats) {
     __shared__ int s_stack[kStackLds * kTraceBlock];
@@ -235,7 +368,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow(DeviceScene sc, PathStat
         float tmax = o.w;
         uint32_t k = 0, idx = 0;
         float b1, b2;
-        const bool occluded = traverse<true, STATS>(sc, r, 0.001f, tmax, k, idx, b1, b2, st, nv, pt);
+        const bool occluded = trace_ray<true, STATS, W>(sc, r, 0.001f, tmax, k, idx, b1, b2, st, nv, pt);
         if (!occluded) {  // main.cu:124-139
             const float4 c = ps.sh_c[p];
             float4 L = ps.rad[p];
@@ -576,8 +709,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_debug(DeviceScene sc, con
     uint32_t key = 0xFFFFFFFFu, idx = kMissIndex, nv = 0, pt = 0;
     float b1 = 0.f, b2 = 0.f;
     bool hit;
-    if (any) hit = traverse<true, false>(sc, r, r8[6], tmax, key, idx, b1, b2, st, nv, pt);
-    else hit = traverse<false, false>(sc, r, r8[6], tmax, key, idx, b1, b2, st, nv, pt);
+    if (sc.bvh_width == 4) {
+        if (any) hit = traverse4<true, false>(sc, r, r8[6], tmax, key, idx, b1, b2, st, nv, pt);
+        else hit = traverse4<false, false>(sc, r, r8[6], tmax, key, idx, b1, b2, st, nv, pt);
+    } else {
+        if (any) hit = traverse<true, false>(sc, r, r8[6], tmax, key, idx, b1, b2, st, nv, pt);
+        else hit = traverse<false, false>(sc, r, r8[6], tmax, key, idx, b1, b2, st, nv, pt);
+    }
     float *o = out + 4 * (size_t)i;
     o[0] = hit ? (any ? 1.f : tmax) : -1.f;
     o[1] = b1;
@@ -624,22 +762,35 @@ void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, 
                    const TraceStats *stats, hipStream_t s) {
     const uint32_t blocks = ovf_threads / kTraceBlock;
     TraceStats st = stats ? *stats : TraceStats{nullptr};
-    if (stats)
-        hipLaunchKernelGGL(k_extend<true>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, queue, queue_count,
-                           static_count, ovf, ovf_threads, st);
-    else
-        hipLaunchKernelGGL(k_extend<false>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, queue, queue_count,
-                           static_count, ovf, ovf_threads, st);
+    const bool w4 = sc.bvh_width == 4;
+#define EXTEND(S, W)                                                                                         \
+    hipLaunchKernelGGL((k_extend<S, W>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, queue, queue_count, \
+                       static_count, ovf, ovf_threads, st)
+    if (stats) {
+        if (w4) EXTEND(true, 4);
+        else EXTEND(true, 2);
+    } else {
+        if (w4) EXTEND(false, 4);
+        else EXTEND(false, 2);
+    }
+#undef EXTEND
 }
 
 void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                    const TraceStats *stats, hipStream_t s) {
     const uint32_t blocks = ovf_threads / kTraceBlock;
     TraceStats st = stats ? *stats : TraceStats{nullptr};
-    if (stats)
-        hipLaunchKernelGGL(k_shadow<true>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, ovf, ovf_threads, st);
-    else
-        hipLaunchKernelGGL(k_shadow<false>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, ovf, ovf_threads, st);
+    const bool w4 = sc.bvh_width == 4;
+#define SHADOW(S, W) \
+    hipLaunchKernelGGL((k_shadow<S, W>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, ovf, ovf_threads, st)
+    if (stats) {
+        if (w4) SHADOW(true, 4);
+        else SHADOW(true, 2);
+    } else {
+        if (w4) SHADOW(false, 4);
+        else SHADOW(false, 2);
+    }
+#undef SHADOW
 }
 
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,

@@ -87,6 +87,20 @@ struct alignas(16) BvhNode {
     float4 hi1;  // xyz = child1 max
 };
 
+// 4-wide node with 8-bit quantized child boxes: 64 B = one half L2 line holds
+// what four 64 B BVH2 nodes spread over two levels.  Child k's box is
+// origin + q * 2^(e-127) per axis; the builder rounds q outward and verifies
+// the decoded float box contains the exact child box (conservative culling).
+struct alignas(64) Bvh4Node {
+    float ox, oy, oz;
+    uint32_t exps;      // e_x | e_y << 8 | e_z << 16 (biased float exponents of the scales)
+    int32_t child[4];   // links (see below); kEmptyLink for unused slots
+    uint32_t qlo_x, qlo_y, qlo_z;  // byte k = child k
+    uint32_t qhi_x, qhi_y, qhi_z;
+    uint32_t pad[2];
+};
+constexpr int kEmptyLink = 0x7FFFFFFF;
+
 // Child link encoding: link >= 0 -> internal node index; link < 0 -> leaf,
 // ~link = (first_prim << 3) | (count - 1), count in [1, 8].
 constexpr int kLeafMax = 8;
@@ -103,9 +117,12 @@ struct Camera {
 
 struct DeviceScene {
     const BvhNode *nodes;
+    const Bvh4Node *nodes4;
     const float4 *prims;  // 3 float4 per primitive, Morton order
     uint32_t num_prims;
-    uint32_t root_link;   // link of the root (internal 0 or a leaf)
+    uint32_t root_link;   // link of the root (internal 0 or a leaf), BVH2
+    uint32_t root_link4;  // same for the BVH4
+    uint32_t bvh_width;   // 2 or 4: which node array the traversal kernels use
     const uint32_t *prim_inst;  // global prim id -> instance
     const DevInstance *instances;
     const DevMaterial *materials;

@@ -76,7 +76,9 @@ def _cornell(res, depth=4):
     return World().load_scene(scenes.cornell_xml(os.path.join(TMP, f"cb{res}.xml"), res, res, depth))
 
 
-def test_primary_hits_match_oracle():
+@pytest.mark.parametrize("width", ["2", "4"])
+def test_primary_hits_match_oracle(width, monkeypatch):
+    monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
     w = _cornell(96)
     desc = w.desc()
     o = oracle.OracleScene(desc)
@@ -133,12 +135,40 @@ def test_materials_parity_config2():
     compare(gpu, ref, "materials192x8")
 
 
-def test_sphere_field_parity():
+@pytest.mark.parametrize("width", ["2", "4"])
+def test_sphere_field_parity(width, monkeypatch):
+    monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
     w = scenes.sphere_field(27, 240, 136, 4, seed=3)
     desc = w.desc()
     gpu = render_gpu(desc, 2)
     ref = oracle.OracleScene(desc).render(spp=2)
-    compare(gpu, ref, "field27")
+    compare(gpu, ref, f"field27-bvh{width}")
+
+
+def test_field_hits_random_rays_both_widths(monkeypatch):
+    """Closest hits of 200k random rays in a 54k-triangle field: BVH2, BVH4 and the oracle agree."""
+    w = scenes.sphere_field(27, 64, 36, 4, seed=9)
+    desc = w.desc()
+    rng = np.random.default_rng(11)
+    org = rng.uniform([-7.5, 0.1, -9.5], [7.5, 13.9, 13.5], (200000, 3))
+    d = rng.normal(size=(200000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([org, d], 1).astype(np.float32)
+    ref = oracle.OracleScene(desc).closest(rays)
+    r8 = np.ascontiguousarray(np.concatenate([rays, np.full((len(rays), 1), 0.001, np.float32),
+                                              np.full((len(rays), 1), 1e16, np.float32)], 1))
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    for width in ("2", "4"):
+        monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+        pt = PTPass(device=0)
+        pt.set_scene(desc)
+        out = np.zeros((len(rays), 4), np.float32)
+        abi.check(pt._lib.pupil_pt_trace_rays(pt._pt, len(rays), r8.ctypes.data_as(abi.f32p),
+                                              out.ctypes.data_as(abi.f32p), 0))
+        bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
+        assert not bad.any(), f"bvh{width}: {bad.sum()} rays differ"
+        pt.close_engine()
 
 
 def test_accumulation_equals_onrun_sequence():
