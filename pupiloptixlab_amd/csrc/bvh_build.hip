@@ -462,7 +462,12 @@ void free_lbvh(BvhBuildOutput &out) {
 
 int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms) {
     const int n = (int)in.num_prims;
-    if (n <= 0) return -1;
+    if (n <= 0) {  // empty scene: every ray misses
+        out = BvhBuildOutput{};
+        out.root_link = out.root_link4 = (uint32_t)kTraverseDone;
+        if (build_ms) *build_ms = 0.0;
+        return 0;
+    }
     if (leaf_size < 1) leaf_size = 1;
     if (leaf_size > (uint32_t)kLeafMax) leaf_size = kLeafMax;
     hipEvent_t e0, e1;
@@ -560,20 +565,20 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     if (build_ms) *build_ms = ms;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    hipFree(recs);
-    hipFree(boxes);
-    hipFree(node_boxes);
-    hipFree(bounds);
-    hipFree(keys);
-    hipFree(vals);
-    hipFree(keys2);
-    hipFree(vals2);
-    hipFree(hist);
-    hipFree(flags);
-    hipFree(children);
-    hipFree(ranges);
-    hipFree(parent_internal);
-    hipFree(parent_leaf);
+    (void)hipFree(recs);
+    (void)hipFree(boxes);
+    (void)hipFree(node_boxes);
+    (void)hipFree(bounds);
+    (void)hipFree(keys);
+    (void)hipFree(vals);
+    (void)hipFree(keys2);
+    (void)hipFree(vals2);
+    (void)hipFree(hist);
+    (void)hipFree(flags);
+    (void)hipFree(children);
+    (void)hipFree(ranges);
+    (void)hipFree(parent_internal);
+    (void)hipFree(parent_leaf);
     return err == hipSuccess ? 0 : -2;
 }
 

@@ -8,6 +8,7 @@
 // pupil_pt_render  = spp x PTPass::OnRun (pt_pass.cpp:39-57) as one wavefront batch.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -434,6 +435,11 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     sc.bvh_width = 4;
     if (const char *w = std::getenv("PUPIL_BVH_WIDTH"))  // A/B switch for the node format
         if (std::atoi(w) == 2) sc.bvh_width = 2;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pt->device);
+    sc.num_cus = (uint32_t)std::max(1, cus);
+    sc.trace_refill = 32;  // persistent BVH4 kernels; 0 selects the one-ray-per-lane kernels (A/B)
+    if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
     sc.prim_inst = d_prim_inst;
     sc.instances = d_insts;
     sc.materials = d_mats;
@@ -552,7 +558,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     launch_extend(pt->sc, pt->ps, pt->q, nullptr, nullptr, fp.num_paths, pt->ovf, pt->ovf_threads, tsp, s);
     ev1();
     for (uint32_t b = 0; b < bounces; b++) {
-        HIP_TRY(hipMemsetAsync(pt->q.counts + 9, 0, 2 * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(pt->q.counts + 9, 0, 4 * sizeof(uint32_t), s));  // next, shadow, 2 work counters
         launch_shade(pt->sc, fp, pt->ps, pt->q, b, s);
         if (b < 128)
             HIP_TRY(hipMemcpyAsync(pt->ray_log + 2 * b, pt->q.counts + 9, 2 * sizeof(uint32_t),
@@ -629,7 +635,10 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
     hipError_t e = hipMalloc((void **)&d_out, sizeof(float) * 4 * (size_t)n);
     if (e == hipSuccess) e = hipMemcpy(d_rays, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        launch_trace_debug(pt->sc, d_rays, d_out, n, any_hit, pt->ovf, pt->ovf_threads, pt->own_stream);
+        e = hipMemsetAsync(pt->q.counts + 13, 0, sizeof(uint32_t), pt->own_stream);
+        if (e == hipSuccess)
+            launch_trace_debug(pt->sc, d_rays, d_out, n, any_hit, pt->ovf, pt->ovf_threads, pt->q.counts + 13,
+                               pt->own_stream);
         e = hipStreamSynchronize(pt->own_stream);
     }
     if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(float) * 4 * (size_t)n, hipMemcpyDeviceToHost);

@@ -9,6 +9,7 @@
 namespace pupil {
 
 constexpr int kTraceBlock = 128;
+constexpr int kTraceWavesPerSimd = 6;  // persistent BVH4 kernels: occupancy target (<= 80 VGPRs)
 constexpr int kStackLds = 32;   // per-thread LDS stack entries
 constexpr int kStackOvf = 96;   // per-thread global overflow entries
 constexpr int kShadeBlock = 256;
@@ -71,7 +72,7 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
 void launch_accumulate(const FrameParams &fp, const PathState &ps, hipStream_t s);
 uint32_t trace_grid_blocks();
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
-                        uint32_t ovf_threads, hipStream_t s);
+                        uint32_t ovf_threads, uint32_t *work, hipStream_t s);
 void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, hipStream_t s);
 
 // LBVH builder (bvh_build.hip)

@@ -19,6 +19,8 @@
 #include "pt_shading.h"
 #include "pt_trace.h"
 
+#include <algorithm>
+
 namespace pupil {
 
 namespace {
@@ -59,7 +61,7 @@ struct Stack {
     }
 };
 
-constexpr int kSentinel = 0x76543210;
+constexpr int kSentinel = kTraverseDone;
 
 // Aila-Laine while-while traversal with postponed leaves.  ANY = shadow
 // (terminate on first hit, OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT).
@@ -71,8 +73,12 @@ __device__ __forceinline__ bool traverse(const DeviceScene &sc, const RayPre &r,
     st.store(0, kSentinel);
     int node = (int)sc.root_link;
     int leaf = 0;
+    if (node < 0) {  // the whole scene is one leaf
+        leaf = node;
+        node = kSentinel;
+    }
     bool found = false;
-    while (node != kSentinel) {
+    while (node != kSentinel || leaf < 0) {
         while ((uint32_t)node < (uint32_t)kSentinel) {
             const BvhNode n = sc.nodes[node];
             if (STATS) nodes_visited++;
@@ -217,8 +223,12 @@ __device__ __forceinline__ bool traverse4(const DeviceScene &sc, const RayPre &r
     st.store(0, kSentinel);
     int node = (int)sc.root_link4;
     int leaf = 0;
+    if (node < 0) {  // the whole scene is one leaf
+        leaf = node;
+        node = kSentinel;
+    }
     bool found = false;
-    while (node != kSentinel) {
+    while (node != kSentinel || leaf < 0) {
         while ((uint32_t)node < (uint32_t)kSentinel) {
             const Bvh4Node n = sc.nodes4[node];
             if (STATS) nodes_visited++;
@@ -379,6 +389,256 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow(DeviceScene sc, PathStat
         }
     }
     flush_stats<STATS>(&stats, nv, pt);
+}
+
+// ------------------------------------------------------------------ persistent 4-wide traversal
+// The production trace kernels for the quantized BVH4.  Waves are persistent
+// and pull rays from the queue with one atomic per wave; a lane whose ray has
+// terminated is refilled as soon as `refill` lanes of its wave are idle
+// (Aila & Laine 2009, "dynamic fetch"), so a wave never idles on its longest
+// ray.  The stack is a 16-entry LDS ring per lane that spills its oldest 8
+// entries to HBM when full, so push/pop are LDS-only in the common case.
+constexpr int kRing = 16;
+constexpr int kSpill = 8;
+static_assert((kRing & (kRing - 1)) == 0, "ring size must be a power of two");
+
+struct RingStack {
+    int *lds;  // this lane's column (stride kTraceBlock)
+    int *ovf;  // this lane's overflow column (stride ovf_stride)
+    uint32_t ovf_stride;
+    int sp;   // logical entries [0, sp)
+    int bot;  // entries [0, bot) live in ovf, [bot, sp) in the ring
+
+    __device__ __forceinline__ int &slot(int i) { return lds[(i & (kRing - 1)) * kTraceBlock]; }
+    __device__ __forceinline__ void reset() { sp = bot = 0; }
+    // Make room for three pushes.  When the overflow column is exhausted too
+    // (stack deeper than kRing + kStackOvf, impossible for trees of depth
+    // <= 32) the oldest entries are overwritten: a wrong answer, never an
+    // out-of-bounds access.
+    __device__ __forceinline__ void reserve3() {
+        if (sp + 3 - bot > kRing && bot + kSpill <= kStackOvf) {
+#pragma unroll
+            for (int k = 0; k < kSpill; k++) ovf[(uint32_t)(bot + k) * ovf_stride] = slot(bot + k);
+            bot += kSpill;
+        }
+    }
+    __device__ __forceinline__ void push(int v, bool keep) {
+        slot(sp) = v;  // harmless above the top when !keep
+        sp += keep ? 1 : 0;
+    }
+    __device__ __forceinline__ int pop() {
+        if (sp == 0) return kSentinel;
+        sp--;
+        if (sp < bot) {
+            bot -= kSpill;
+#pragma unroll
+            for (int k = 0; k < kSpill; k++) slot(bot + k) = ovf[(uint32_t)(bot + k) * ovf_stride];
+        }
+        return slot(sp);
+    }
+};
+
+// Branch-free compare-exchange (selects, no divergent swap blocks).
+__device__ __forceinline__ void csel(float &ta, int &la, float &tb, int &lb) {
+    const bool c = tb < ta;
+    const float t0 = c ? tb : ta, t1 = c ? ta : tb;
+    const int l0 = c ? lb : la, l1 = c ? la : lb;
+    ta = t0;
+    tb = t1;
+    la = l0;
+    lb = l1;
+}
+
+enum TraceMode : int { kModeExtend = 0, kModeShadow = 1, kModeRays = 2 };
+
+struct TraceJob {
+    const uint32_t *queue;      // extend: path ids (null = identity)
+    const uint32_t *count_ptr;  // device count (null = static_count)
+    uint32_t static_count;
+    uint32_t *work;             // work counter, zero at launch
+    uint32_t refill;            // refill when at least this many lanes are idle (1..64)
+    const float *rays;          // kModeRays: 8 floats per ray (o, d, tmin, tmax)
+    float *out;                 // kModeRays: 4 floats per ray
+};
+
+// One node of the quantized BVH4: child boxes decoded exactly as the builder
+// verified them (origin + q * 2^e; the product is exact, so the fma rounds
+// once like the builder's sum), near/far planes picked by the ray's direction
+// signs (equal to the min/max of the two slabs), conservative far distance.
+__device__ __forceinline__ void visit4(const Bvh4Node &n, const RayPre &r, float tmin, float tmax, float t[4],
+                                       int l[4]) {
+    constexpr float kInf = __builtin_huge_valf();
+    const float sx = __uint_as_float((n.exps & 0xFFu) << 23);
+    const float sy = __uint_as_float(((n.exps >> 8) & 0xFFu) << 23);
+    const float sz = __uint_as_float(((n.exps >> 16) & 0xFFu) << 23);
+    const bool px = r.idir.x >= 0.f, py = r.idir.y >= 0.f, pz = r.idir.z >= 0.f;
+    const uint32_t nx = px ? n.qlo_x : n.qhi_x, fx = px ? n.qhi_x : n.qlo_x;
+    const uint32_t ny = py ? n.qlo_y : n.qhi_y, fy = py ? n.qhi_y : n.qlo_y;
+    const uint32_t nz = pz ? n.qlo_z : n.qhi_z, fz = pz ? n.qhi_z : n.qlo_z;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float bnx = __builtin_fmaf((float)((nx >> (8 * k)) & 0xFFu), sx, n.ox);
+        const float bfx = __builtin_fmaf((float)((fx >> (8 * k)) & 0xFFu), sx, n.ox);
+        const float bny = __builtin_fmaf((float)((ny >> (8 * k)) & 0xFFu), sy, n.oy);
+        const float bfy = __builtin_fmaf((float)((fy >> (8 * k)) & 0xFFu), sy, n.oy);
+        const float bnz = __builtin_fmaf((float)((nz >> (8 * k)) & 0xFFu), sz, n.oz);
+        const float bfz = __builtin_fmaf((float)((fz >> (8 * k)) & 0xFFu), sz, n.oz);
+        const float tn = fmaxf(fmaxf(fmaxf((bnx - r.o.x) * r.idir.x, (bny - r.o.y) * r.idir.y),
+                                     (bnz - r.o.z) * r.idir.z),
+                               tmin);
+        float tf = fminf(fminf(fminf((bfx - r.o.x) * r.idir.x, (bfy - r.o.y) * r.idir.y), (bfz - r.o.z) * r.idir.z),
+                         tmax);
+        tf = tf * kBoxConservative;
+        l[k] = n.child[k];
+        t[k] = (tn <= tf && l[k] != kEmptyLink) ? tn : kInf;
+    }
+    csel(t[0], l[0], t[1], l[1]);
+    csel(t[2], l[2], t[3], l[3]);
+    csel(t[0], l[0], t[2], l[2]);
+    csel(t[1], l[1], t[3], l[3]);
+    csel(t[1], l[1], t[2], l[2]);
+}
+
+template <int MODE, bool ANY, bool STATS>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4(DeviceScene sc, PathState ps, Queues q, TraceJob job,
+                                                        int *ovf, uint32_t ovf_threads, TraceStats stats) {
+    constexpr float kInf = __builtin_huge_valf();
+    __shared__ int s_ring[kRing * kTraceBlock];
+    const uint32_t count = MODE == kModeShadow ? q.counts[10] : (job.count_ptr ? *job.count_ptr : job.static_count);
+    RingStack st;
+    st.lds = s_ring + threadIdx.x;
+    st.ovf = ovf + blockIdx.x * blockDim.x + threadIdx.x;
+    st.ovf_stride = ovf_threads;
+    st.reset();
+    uint32_t nv = 0, npt = 0;
+    bool active = false, drained = false;
+    uint32_t p = 0, best_key = 0, best_idx = kMissIndex;
+    RayPre r{};
+    float tmin = 0.f, tmax = 0.f, b1 = 0.f, b2 = 0.f;
+    int node = kSentinel, leaf = 0;
+    bool found = false;
+    for (;;) {
+        // ---- refill idle lanes (one atomic per wave)
+        const unsigned long long idle = __ballot(!active);
+        const uint32_t n_idle = (uint32_t)__popcll(idle);
+        if (!drained && n_idle >= job.refill) {
+            uint32_t base = 0;
+            if (lane_id() == 0) base = atomicAdd(job.work, n_idle);
+            base = __shfl(base, 0);
+            if (base + n_idle >= count) drained = true;
+            if (!active) {
+                const uint32_t i = base + (uint32_t)__popcll(idle & lanemask_lt());
+                if (i < count) {
+                    float4 o, d;
+                    if (MODE == kModeExtend) {
+                        p = job.queue ? job.queue[i] : i;
+                        o = ps.ray_o[p];
+                        d = ps.ray_d[p];
+                        tmin = 0.001f;
+                        tmax = kMaxDistance;
+                    } else if (MODE == kModeShadow) {
+                        p = q.shadow[i];
+                        o = ps.sh_o[p];
+                        d = ps.sh_d[p];
+                        tmin = 0.001f;
+                        tmax = o.w;
+                    } else {
+                        p = i;
+                        const float *r8 = job.rays + 8 * (size_t)i;
+                        o = make_float4(r8[0], r8[1], r8[2], 0.f);
+                        d = make_float4(r8[3], r8[4], r8[5], 0.f);
+                        tmin = r8[6];
+                        tmax = r8[7];
+                    }
+                    r = ray_pre(f3(o), f3(d));
+                    best_key = 0xFFFFFFFFu;
+                    best_idx = kMissIndex;
+                    b1 = b2 = 0.f;
+                    found = false;
+                    st.reset();
+                    node = (int)sc.root_link4;
+                    leaf = 0;
+                    if (node < 0) {
+                        leaf = node;
+                        node = kSentinel;
+                    }
+                    active = true;
+                }
+            }
+        }
+        if (!__any(active)) {
+            if (drained) break;
+            continue;
+        }
+        // ---- traverse until this lane's ray terminates or it needs a leaf while others do too
+        if (active) {
+            while ((uint32_t)node < (uint32_t)kSentinel) {
+                const Bvh4Node n = sc.nodes4[node];
+                if (STATS) nv++;
+                float t[4];
+                int l[4];
+                visit4(n, r, tmin, tmax, t, l);
+                if (t[0] == kInf) {
+                    node = st.pop();
+                } else {
+                    node = l[0];
+                    st.reserve3();
+                    st.push(l[3], t[3] != kInf);
+                    st.push(l[2], t[2] != kInf);
+                    st.push(l[1], t[1] != kInf);
+                }
+                if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
+                    leaf = node;
+                    node = st.pop();
+                }
+                if (!__any(leaf >= 0)) break;
+            }
+            while (leaf < 0) {
+                if (intersect_leaf<ANY, STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, npt, found))
+                    break;
+                leaf = node;
+                if (node < 0) node = st.pop();
+            }
+        }
+        const bool done = active && ((node == kSentinel && leaf >= 0) || (ANY && found));
+        // ---- retire
+        if (MODE == kModeExtend) {
+            uint32_t bin = 0;
+            if (done) {
+                ps.hit[p] = make_float4(found ? tmax : -1.f, b1, b2, __uint_as_float(found ? best_idx : kMissIndex));
+                if (found) {
+                    const uint32_t mt = __float_as_uint(sc.prims[3 * best_idx + 2].w);
+                    bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
+                }
+            }
+            bool pending = done;
+            while (__any(pending)) {
+                const unsigned long long m = __ballot(pending);
+                const int leader = __ffsll((long long)m) - 1;
+                const uint32_t b = __shfl(bin, leader);
+                const bool mine = pending && bin == b;
+                wave_append(mine, p, q.bins + (size_t)b * q.capacity, q.counts + b);
+                if (mine) pending = false;
+            }
+        } else if (MODE == kModeShadow) {
+            if (done && !found) {  // main.cu:124-139
+                const float4 c = ps.sh_c[p];
+                float4 L = ps.rad[p];
+                L.x = L.x + c.x;
+                L.y = L.y + c.y;
+                L.z = L.z + c.z;
+                ps.rad[p] = L;
+            }
+        } else if (done) {
+            float *o = job.out + 4 * (size_t)p;
+            o[0] = found ? (ANY ? 1.f : tmax) : -1.f;
+            o[1] = b1;
+            o[2] = b2;
+            o[3] = __uint_as_float(found && !ANY ? best_key : 0xFFFFFFFFu);
+        }
+        if (done) active = false;
+    }
+    flush_stats<STATS>(&stats, nv, npt);
 }
 
 // ------------------------------------------------------------------ generate
@@ -739,8 +999,25 @@ __global__ void k_debug_math(const float *x, const float *y2, float *out, uint32
 
 }  // namespace
 
+// Persistent grid: exactly the resident capacity (CUs x 4 SIMDs x waves per SIMD).
+static uint32_t trace4_blocks(const DeviceScene &sc, uint32_t ovf_threads) {
+    const uint32_t resident = sc.num_cus * 4u * (uint32_t)kTraceWavesPerSimd / (kTraceBlock / 64u);
+    return std::min(ovf_threads / kTraceBlock, std::max(1u, resident));
+}
+
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
-                        uint32_t ovf_threads, hipStream_t s) {
+                        uint32_t ovf_threads, uint32_t *work, hipStream_t s) {
+    if (sc.bvh_width == 4 && sc.trace_refill) {  // the production kernel, fed from a ray array
+        const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, rays, out};
+        const uint32_t blocks = trace4_blocks(sc, ovf_threads);
+        if (any)
+            hipLaunchKernelGGL((k_trace4<kModeRays, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
+                               PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
+        else
+            hipLaunchKernelGGL((k_trace4<kModeRays, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
+                               PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
+        return;
+    }
     hipLaunchKernelGGL(k_trace_debug, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, s, sc, rays,
                        out, n, any, ovf, ovf_threads);
 }
@@ -763,7 +1040,18 @@ void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     const uint32_t blocks = ovf_threads / kTraceBlock;
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
-#define EXTEND(S, W)                                                                                         \
+    if (w4 && sc.trace_refill) {
+        const TraceJob job{queue, queue_count, static_count, q.counts + 11, sc.trace_refill, nullptr, nullptr};
+        const uint32_t blocks = trace4_blocks(sc, ovf_threads);
+        if (stats)
+            hipLaunchKernelGGL((k_trace4<kModeExtend, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
+                               job, ovf, ovf_threads, st);
+        else
+            hipLaunchKernelGGL((k_trace4<kModeExtend, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps,
+                               q, job, ovf, ovf_threads, st);
+        return;
+    }
+#define EXTEND(S, W)                                                                                      \
     hipLaunchKernelGGL((k_extend<S, W>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, queue, queue_count, \
                        static_count, ovf, ovf_threads, st)
     if (stats) {
@@ -781,7 +1069,18 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     const uint32_t blocks = ovf_threads / kTraceBlock;
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
-#define SHADOW(S, W) \
+    if (w4 && sc.trace_refill) {
+        const TraceJob job{nullptr, nullptr, 0u, q.counts + 12, sc.trace_refill, nullptr, nullptr};
+        const uint32_t blocks = trace4_blocks(sc, ovf_threads);
+        if (stats)
+            hipLaunchKernelGGL((k_trace4<kModeShadow, true, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
+                               job, ovf, ovf_threads, st);
+        else
+            hipLaunchKernelGGL((k_trace4<kModeShadow, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
+                               job, ovf, ovf_threads, st);
+        return;
+    }
+#define SHADOW(S, W)\
     hipLaunchKernelGGL((k_shadow<S, W>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, ovf, ovf_threads, st)
     if (stats) {
         if (w4) SHADOW(true, 4);

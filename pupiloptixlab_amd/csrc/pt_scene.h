@@ -100,6 +100,9 @@ struct alignas(64) Bvh4Node {
     uint32_t pad[2];
 };
 constexpr int kEmptyLink = 0x7FFFFFFF;
+// Traversal terminator (stack bottom); also the root link of an empty scene.
+// Inner-node links are < kTraverseDone, leaf links are negative.
+constexpr int kTraverseDone = 0x76543210;
 
 // Child link encoding: link >= 0 -> internal node index; link < 0 -> leaf,
 // ~link = (first_prim << 3) | (count - 1), count in [1, 8].
@@ -123,6 +126,8 @@ struct DeviceScene {
     uint32_t root_link;   // link of the root (internal 0 or a leaf), BVH2
     uint32_t root_link4;  // same for the BVH4
     uint32_t bvh_width;   // 2 or 4: which node array the traversal kernels use
+    uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
+    uint32_t num_cus;       // compute units of the device (persistent grid size)
     const uint32_t *prim_inst;  // global prim id -> instance
     const DevInstance *instances;
     const DevMaterial *materials;

@@ -12,6 +12,7 @@ import pytest
 
 import oracle
 from pupiloptixlab_amd import World, scenes
+from pupiloptixlab_amd import world as world_mod
 from pupiloptixlab_amd import abi
 
 pytestmark = pytest.mark.gpu
@@ -145,8 +146,26 @@ def test_sphere_field_parity(width, monkeypatch):
     compare(gpu, ref, f"field27-bvh{width}")
 
 
-def test_field_hits_random_rays_both_widths(monkeypatch):
-    """Closest hits of 200k random rays in a 54k-triangle field: BVH2, BVH4 and the oracle agree."""
+# (PUPIL_BVH_WIDTH, PUPIL_REFILL): BVH2, BVH4 one-ray-per-lane, BVH4 persistent with several refill thresholds
+TRAVERSALS = [("2", "16"), ("4", "0"), ("4", "1"), ("4", "16"), ("4", "64")]
+
+
+def _trace(desc, rays, any_hit=0, tmin=0.001, tmax=1e16):
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    r8 = np.ascontiguousarray(np.concatenate([rays, np.full((len(rays), 1), tmin, np.float32),
+                                              np.full((len(rays), 1), tmax, np.float32)], 1), np.float32)
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    out = np.zeros((len(rays), 4), np.float32)
+    abi.check(pt._lib.pupil_pt_trace_rays(pt._pt, len(rays), r8.ctypes.data_as(abi.f32p),
+                                          out.ctypes.data_as(abi.f32p), any_hit))
+    pt.close_engine()
+    return out
+
+
+def test_field_hits_random_rays_all_traversals(monkeypatch):
+    """Closest hits of 200k random rays in a 54k-triangle field: every traversal kernel and the oracle agree."""
     w = scenes.sphere_field(27, 64, 36, 4, seed=9)
     desc = w.desc()
     rng = np.random.default_rng(11)
@@ -155,20 +174,80 @@ def test_field_hits_random_rays_both_widths(monkeypatch):
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.concatenate([org, d], 1).astype(np.float32)
     ref = oracle.OracleScene(desc).closest(rays)
-    r8 = np.ascontiguousarray(np.concatenate([rays, np.full((len(rays), 1), 0.001, np.float32),
-                                              np.full((len(rays), 1), 1e16, np.float32)], 1))
-    from pupiloptixlab_amd.pt_pass import PTPass
-
-    for width in ("2", "4"):
+    for width, refill in TRAVERSALS:
         monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
-        pt = PTPass(device=0)
-        pt.set_scene(desc)
-        out = np.zeros((len(rays), 4), np.float32)
-        abi.check(pt._lib.pupil_pt_trace_rays(pt._pt, len(rays), r8.ctypes.data_as(abi.f32p),
-                                              out.ctypes.data_as(abi.f32p), 0))
+        monkeypatch.setenv("PUPIL_REFILL", refill)
+        out = _trace(desc, rays)
         bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
-        assert not bad.any(), f"bvh{width}: {bad.sum()} rays differ"
-        pt.close_engine()
+        assert not bad.any(), f"bvh{width} refill {refill}: {bad.sum()} rays differ"
+        occ = _trace(desc, rays, any_hit=1)
+        assert np.array_equal(occ[:, 0] > 0, ref[:, 0] > 0), f"bvh{width} refill {refill}: any-hit differs"
+
+
+def _quad_stack(n, spacing=0.01):
+    """n parallel unit quads stacked along z: every ray along z crosses all of them, so the
+    traversal stack grows past the 16-entry LDS ring and spills to HBM."""
+    w = World()
+    z = np.arange(n, dtype=np.float32) * spacing
+    pos = np.zeros((n, 4, 3), np.float32)
+    pos[:, :, 0] = [-1, 1, 1, -1]
+    pos[:, :, 1] = [-1, -1, 1, 1]
+    pos[:, :, 2] = z[:, None]
+    idx = (np.arange(n, dtype=np.uint32)[:, None] * 4 + np.array([0, 1, 2, 0, 2, 3], np.uint32)).reshape(-1, 3)
+    s = w.add_mesh(pos.reshape(-1, 3), idx)
+    m = w.add_material(world_mod.diffuse((0.5, 0.5, 0.5)))
+    w.add_instance(s, m)
+    w.set_film(16, 16, 2)
+    w.set_sensor(40.0, world_mod.look_at_mitsuba((0, 0, -3), (0, 0, 0), (0, 1, 0)))
+    return w
+
+
+def test_deep_stack_spills_match_oracle(monkeypatch):
+    w = _quad_stack(6000)
+    desc = w.desc()
+    rng = np.random.default_rng(5)
+    n = 20000
+    org = np.concatenate([rng.uniform(-0.9, 0.9, (n, 2)), np.full((n, 1), -1.0)], 1)
+    d = np.concatenate([rng.uniform(-0.02, 0.02, (n, 2)), np.ones((n, 1))], 1)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    # half the rays start inside the stack and go backwards (farthest-first order)
+    org[n // 2:, 2] = 70.0
+    d[n // 2:, 2] *= -1
+    rays = np.concatenate([org, d], 1).astype(np.float32)
+    ref = oracle.OracleScene(desc).closest(rays)
+    assert (ref[:, 0] > 0).mean() > 0.9
+    for width, refill in TRAVERSALS:
+        monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+        monkeypatch.setenv("PUPIL_REFILL", refill)
+        out = _trace(desc, rays)
+        bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
+        assert not bad.any(), f"bvh{width} refill {refill}: {bad.sum()} rays differ"
+
+
+@pytest.mark.parametrize("ntri", [1, 2, 4, 5])
+def test_tiny_scenes(ntri, monkeypatch):
+    """The root is a leaf (<= 4 primitives): traversal terminates and hits match."""
+    w = World()
+    tri_pos = np.array([[-1, -1, 0], [1, -1, 0], [0, 1, 0]], np.float32)
+    pos = np.concatenate([tri_pos + [0, 0, 0.1 * k] for k in range(ntri)]).astype(np.float32)
+    s = w.add_mesh(pos, np.arange(3 * ntri, dtype=np.uint32).reshape(-1, 3))
+    w.add_instance(s, w.add_material(world_mod.diffuse((0.5, 0.5, 0.5))))
+    w.set_film(16, 16, 2)
+    w.set_sensor(40.0, world_mod.look_at_mitsuba((0, 0, -3), (0, 0, 0), (0, 1, 0)))
+    desc = w.desc()
+    rng = np.random.default_rng(2)
+    org = np.concatenate([rng.uniform(-1, 1, (500, 2)), np.full((500, 1), -2.0)], 1)
+    d = np.concatenate([rng.uniform(-0.2, 0.2, (500, 2)), np.ones((500, 1))], 1)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([org, d], 1).astype(np.float32)
+    ref = oracle.OracleScene(desc).closest(rays)
+    for width, refill in TRAVERSALS:
+        monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+        monkeypatch.setenv("PUPIL_REFILL", refill)
+        out = _trace(desc, rays)
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), f"bvh{width} refill {refill}"
+    gpu = render_gpu(desc, 1)
+    assert np.isfinite(gpu["pt accum buffer"]).all()
 
 
 def test_accumulation_equals_onrun_sequence():
