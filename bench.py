@@ -108,14 +108,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    trace_ms = 0.0
-    trace_launches = 0
+    ext_ms = trace_ms = shade_ms = 0.0
+    ext_launches = 0
     rays_local = 0
     for _ in range(args.steps):
         frame()
         st = pt.stats()  # waits for the frame's end event
+        ext_ms += st["extend_ms"]
+        ext_launches += st["extend_launches"]
         trace_ms += st["trace_ms"]
-        trace_launches += st["trace_launches"]
+        shade_ms += st["shade_ms"]
         rays_local += st["primary_rays"] + st["extension_rays"] + st["shadow_rays"]
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -136,11 +138,15 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     mrays = rays_total / elapsed / 1e6
     rays_frame_local = st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"]
-    # roofline: traversal kernels (k_extend + k_shadow), algorithmic bytes per
-    # 32 B ray + 16 B hit + 64 B/node visit + 48 B/prim test
-    per_launch_bytes = st_bytes["trace_bytes"] / max(1, st_bytes["trace_launches"])
-    per_launch_ms = trace_ms / max(1, trace_launches)
+    # roofline of the dominant kernel, the closest-hit traversal (extend):
+    # algorithmic bytes per SURVEY.md §8(d) = 32 B ray + 16 B hit + 64 B per
+    # node visit + 48 B per primitive test, counted in the instrumented frame,
+    # per launch; divided by the average extend launch time measured with HIP
+    # events on the render stream over the timed frames
+    per_launch_bytes = st_bytes["extend_bytes"] / max(1, st_bytes["extend_launches"])
+    per_launch_ms = ext_ms / max(1, ext_launches)
     achieved_gbs = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
+    traffic = pmc_traffic(args)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
@@ -172,10 +178,13 @@ def main():
                        "path_samples_per_s": round(args.width * args.height * args.spp / (ms_per_step * 1e-3), 1),
                        "bvh_build_ms": round(st_bytes["build_ms"], 3),
                        "avg_node_visits_per_ray": round(st_bytes["node_visits"] / max(1, rays_frame_local), 2),
-                       "avg_prim_tests_per_ray": round(st_bytes["prim_tests"] / max(1, rays_frame_local), 2)},
+                       "avg_prim_tests_per_ray": round(st_bytes["prim_tests"] / max(1, rays_frame_local), 2),
+                       "stage_ms_per_frame": {"extend": round(ext_ms / args.steps, 3),
+                                              "shadow": round((trace_ms - ext_ms) / args.steps, 3),
+                                              "shade": round(shade_ms / args.steps, 3)}},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "k_extend+k_shadow (BVH traversal)",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_trace4<extend> (closest-hit BVH4 traversal)",
                          "bytes_per_launch": round(per_launch_bytes, 1),
                          "ms_per_launch": round(per_launch_ms, 4)},
             "cpu_baseline": cpu,
@@ -183,6 +192,22 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(args):
+    """roofline.traffic: L2->fabric bytes per extend launch measured by the PMC
+    passes of this same command (tools/gpu_pmc.sh -> tools/pmc_summary.py
+    --json), committed as profiles/pmc_extend.json; null when absent or taken
+    on another configuration."""
+    path = os.path.join(HERE, "profiles", "pmc_extend.json")
+    default_cfg = (args.spheres, args.width, args.height, args.spp, args.max_depth) == (500, 1920, 1080, 8, 4)
+    if not default_cfg or not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return round(float(json.load(f)["traffic_bytes_per_launch"]), 1)
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def cpu_baseline(desc, args):

@@ -213,6 +213,14 @@ typedef struct pupil_pt_counters {
     double trace_ms;         /* device time of the traversal kernels in the last render */
     double trace_bytes;      /* algorithmic bytes of the traversal kernels (collect_stats) */
     uint64_t trace_launches;
+    /* the dominant kernel (closest-hit extend) on its own: device time, launches,
+     * and with collect_stats its node visits / primitive tests / algorithmic bytes */
+    double extend_ms;
+    uint64_t extend_launches;
+    uint64_t extend_node_visits;
+    uint64_t extend_prim_tests;
+    double extend_bytes;
+    double shade_ms;         /* device time of the shade stages (all materials) */
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;

@@ -106,6 +106,7 @@ struct pupil_pt {
     uint32_t last_paths = 0, last_bounces = 0;
     bool last_stats = false;
     std::vector<hipEvent_t> trace_events;  // pairs
+    std::vector<uint8_t> pair_kind;        // per pair: 0 extend, 1 shadow, 2 shade
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     uint32_t trace_pairs = 0;
     pupil_pt_counters totals{};
@@ -440,6 +441,8 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     sc.num_cus = (uint32_t)std::max(1, cus);
     sc.trace_refill = 32;  // persistent BVH4 kernels; 0 selects the one-ray-per-lane kernels (A/B)
     if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
+    sc.trace_node_min = 1;
+    if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     sc.prim_inst = d_prim_inst;
     sc.instances = d_insts;
     sc.materials = d_mats;
@@ -452,7 +455,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     std::memcpy(sc.camera.c2w, scene->camera_to_world, sizeof(sc.camera.c2w));
     // traversal overflow stacks, counters, events
     pt->ovf_threads = trace_grid_blocks() * (uint32_t)kTraceBlock;
-    if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 2) ||
+    if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 16) ||
         pt->alloc(&pt->ray_log, 2 * 130) || pt->alloc(&pt->q.counts, 16))
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
@@ -535,40 +538,46 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     TraceStats ts_dev{pt->trace_counters};
     const TraceStats *tsp = stats ? &ts_dev : nullptr;
     const uint32_t bounces = fp.max_depth;
-    // events: begin/end + one pair per trace launch
-    const uint32_t pairs_needed = 2 * bounces + 1;
+    // events: begin/end + one pair per stage launch (kind 0 extend, 1 shadow, 2 shade)
+    const uint32_t pairs_needed = 3 * bounces + 1;
     while (pt->trace_events.size() < 2 * pairs_needed) {
         hipEvent_t e;
         HIP_TRY(hipEventCreate(&e));
         pt->trace_events.push_back(e);
     }
+    pt->pair_kind.assign(pairs_needed, 0);
     uint32_t pair = 0;
-    auto ev0 = [&]() { (void)hipEventRecord(pt->trace_events[2 * pair], s); };
+    auto ev0 = [&](uint8_t kind) {
+        pt->pair_kind[pair] = kind;
+        (void)hipEventRecord(pt->trace_events[2 * pair], s);
+    };
     auto ev1 = [&]() {
         (void)hipEventRecord(pt->trace_events[2 * pair + 1], s);
         pair++;
     };
 
     HIP_TRY(hipEventRecord(pt->ev_begin, s));
-    if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 2 * sizeof(unsigned long long), s));
+    if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 16 * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(pt->ray_log, 0, sizeof(uint32_t) * 2 * 130, s));
     launch_generate(pt->sc, fp, pt->ps, s);
     HIP_TRY(hipMemsetAsync(pt->q.counts, 0, 16 * sizeof(uint32_t), s));
-    ev0();
+    ev0(0);
     launch_extend(pt->sc, pt->ps, pt->q, nullptr, nullptr, fp.num_paths, pt->ovf, pt->ovf_threads, tsp, s);
     ev1();
     for (uint32_t b = 0; b < bounces; b++) {
         HIP_TRY(hipMemsetAsync(pt->q.counts + 9, 0, 4 * sizeof(uint32_t), s));  // next, shadow, 2 work counters
+        ev0(2);
         launch_shade(pt->sc, fp, pt->ps, pt->q, b, s);
+        ev1();
         if (b < 128)
             HIP_TRY(hipMemcpyAsync(pt->ray_log + 2 * b, pt->q.counts + 9, 2 * sizeof(uint32_t),
                                    hipMemcpyDeviceToDevice, s));
         if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
-            ev0();
+            ev0(1);
             launch_shadow(pt->sc, pt->ps, pt->q, pt->ovf, pt->ovf_threads, tsp, s);
             ev1();
             HIP_TRY(hipMemsetAsync(pt->q.counts, 0, 9 * sizeof(uint32_t), s));
-            ev0();
+            ev0(0);
             launch_extend(pt->sc, pt->ps, pt->q, pt->q.next, pt->q.counts + 9, 0u, pt->ovf, pt->ovf_threads, tsp, s);
             ev1();
         }
@@ -602,22 +611,41 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, pt->ev_begin, pt->ev_end));
         c.last_render_ms = ms;
-        double tms = 0.0;
+        double kind_ms[3] = {0.0, 0.0, 0.0};
+        uint64_t kind_n[3] = {0, 0, 0};
         for (uint32_t i = 0; i < pt->trace_pairs; i++) {
             float m = 0.f;
             HIP_TRY(hipEventElapsedTime(&m, pt->trace_events[2 * i], pt->trace_events[2 * i + 1]));
-            tms += m;
+            kind_ms[pt->pair_kind[i]] += m;
+            kind_n[pt->pair_kind[i]]++;
         }
-        c.trace_ms = tms;
-        c.trace_launches = pt->trace_pairs;
+        c.trace_ms = kind_ms[0] + kind_ms[1];
+        c.trace_launches = kind_n[0] + kind_n[1];
+        c.extend_ms = kind_ms[0];
+        c.extend_launches = kind_n[0];
+        c.shade_ms = kind_ms[2];
         if (pt->last_stats) {
-            unsigned long long tc[2];
+            unsigned long long tc[16];
             HIP_TRY(hipMemcpy(tc, pt->trace_counters, sizeof(tc), hipMemcpyDeviceToHost));
-            c.node_visits = tc[0];
-            c.prim_tests = tc[1];
+            for (int k = 0; k < 2 && std::getenv("PUPIL_TRACE_DIAG"); k++) {  // SIMD efficiency, persistent kernels
+                const unsigned long long *d = tc + 2 + 6 * k;
+                if (!d[0]) continue;
+                std::fprintf(stderr,
+                             "[pupil] %s: node loop %llu wave-iters, %.1f%% lanes active; leaf loop %llu wave-iters, "
+                             "%.1f%% lanes active; %llu refills, %.1f lanes each\n",
+                             k ? "shadow" : "extend", d[0], 100.0 * (double)d[1] / (64.0 * (double)d[0]), d[2],
+                             100.0 * (double)d[3] / (64.0 * (double)std::max(1ull, d[2])), d[4],
+                             (double)d[5] / (double)std::max(1ull, d[4]));
+            }
+            c.node_visits = tc[0] + tc[14];
+            c.prim_tests = tc[1] + tc[15];
+            c.extend_node_visits = tc[0];
+            c.extend_prim_tests = tc[1];
             const double rays = (double)(c.primary_rays + c.extension_rays + c.shadow_rays);
             // 32 B ray read + 16 B hit write + 64 B per node + 48 B per primitive
-            c.trace_bytes = rays * 48.0 + 64.0 * (double)tc[0] + 48.0 * (double)tc[1];
+            c.trace_bytes = rays * 48.0 + 64.0 * (double)c.node_visits + 48.0 * (double)c.prim_tests;
+            c.extend_bytes = (double)(c.primary_rays + c.extension_rays) * 48.0 + 64.0 * (double)tc[0] +
+                             48.0 * (double)tc[1];
         }
     }
     *out = c;

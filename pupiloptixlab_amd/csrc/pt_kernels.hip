@@ -291,8 +291,9 @@ __device__ __forceinline__ bool trace_ray(const DeviceScene &sc, const RayPre &r
     else return traverse<ANY, STATS>(sc, r, tmin, tmax, best_key, best_idx, bb1, bb2, st, nv, pt);
 }
 
+// counters[0..1]: closest-hit (extend / ray queries), counters[14..15]: shadow
 template <bool STATS>
-__device__ __forceinline__ void flush_stats(const TraceStats *stats, uint32_t nv, uint32_t pt) {
+__device__ __forceinline__ void flush_stats(const TraceStats *stats, uint32_t nv, uint32_t pt, int base = 0) {
     if (!STATS) return;
     // wave reduction then one atomic per wave
     unsigned long long a = nv, b = pt;
@@ -301,8 +302,8 @@ __device__ __forceinline__ void flush_stats(const TraceStats *stats, uint32_t nv
         b += __shfl_xor(b, o);
     }
     if (lane_id() == 0) {
-        atomicAdd(&stats->counters[0], a);
-        atomicAdd(&stats->counters[1], b);
+        atomicAdd(&stats->counters[base + 0], a);
+        atomicAdd(&stats->counters[base + 1], b);
     }
 }
 
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow(DeviceScene sc, PathStat
             ps.rad[p] = L;
         }
     }
-    flush_stats<STATS>(&stats, nv, pt);
+    flush_stats<STATS>(&stats, nv, pt, 14);
 }
 
 // ------------------------------------------------------------------ persistent 4-wide traversal
@@ -457,6 +458,7 @@ struct TraceJob {
     uint32_t static_count;
     uint32_t *work;             // work counter, zero at launch
     uint32_t refill;            // refill when at least this many lanes are idle (1..64)
+    uint32_t node_min;          // node phase ends when fewer lanes than this still need a node (>= 1)
     const float *rays;          // kModeRays: 8 floats per ray (o, d, tmin, tmax)
     float *out;                 // kModeRays: 4 floats per ray
 };
@@ -511,6 +513,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     st.ovf_stride = ovf_threads;
     st.reset();
     uint32_t nv = 0, npt = 0;
+    // STATS-only SIMD-efficiency diagnostics, each event counted by one lane:
+    // node-loop wave iterations / active lanes, leaf-loop iterations / active
+    // lanes, refills / lanes refilled
+    unsigned long long dg[6] = {0, 0, 0, 0, 0, 0};
     bool active = false, drained = false;
     uint32_t p = 0, best_key = 0, best_idx = kMissIndex;
     RayPre r{};
@@ -525,6 +531,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
             uint32_t base = 0;
             if (lane_id() == 0) base = atomicAdd(job.work, n_idle);
             base = __shfl(base, 0);
+            if (STATS && lane_id() == 0) {
+                dg[4]++;
+                dg[5] += min(n_idle, base < count ? count - base : 0u);
+            }
             if (base + n_idle >= count) drained = true;
             if (!active) {
                 const uint32_t i = base + (uint32_t)__popcll(idle & lanemask_lt());
@@ -574,7 +584,14 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
         if (active) {
             while ((uint32_t)node < (uint32_t)kSentinel) {
                 const Bvh4Node n = sc.nodes4[node];
-                if (STATS) nv++;
+                if (STATS) {
+                    nv++;
+                    const unsigned long long m = __ballot(true);
+                    if ((int)lane_id() == __ffsll((long long)m) - 1) {
+                        dg[0]++;
+                        dg[1] += (unsigned long long)__popcll(m);
+                    }
+                }
                 float t[4];
                 int l[4];
                 visit4(n, r, tmin, tmax, t, l);
@@ -591,9 +608,17 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                     leaf = node;
                     node = st.pop();
                 }
-                if (!__any(leaf >= 0)) break;
+                // leave for the leaf phase once fewer than node_min lanes still need a node
+                if ((uint32_t)__popcll(__ballot(leaf >= 0)) < job.node_min) break;
             }
             while (leaf < 0) {
+                if (STATS) {
+                    const unsigned long long m = __ballot(true);
+                    if ((int)lane_id() == __ffsll((long long)m) - 1) {
+                        dg[2]++;
+                        dg[3] += (unsigned long long)__popcll(m);
+                    }
+                }
                 if (intersect_leaf<ANY, STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, npt, found))
                     break;
                 leaf = node;
@@ -638,7 +663,16 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
         }
         if (done) active = false;
     }
-    flush_stats<STATS>(&stats, nv, npt);
+    flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
+    if (STATS) {
+        for (int k = 0; k < 6; k++) {
+            unsigned long long v = dg[k];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            dg[k] = v;
+        }
+        if (lane_id() == 0)
+            for (int k = 0; k < 6; k++) atomicAdd(&stats.counters[(MODE == kModeShadow ? 8 : 2) + k], dg[k]);
+    }
 }
 
 // ------------------------------------------------------------------ generate
@@ -1008,7 +1042,7 @@ static uint32_t trace4_blocks(const DeviceScene &sc, uint32_t ovf_threads) {
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
                         uint32_t ovf_threads, uint32_t *work, hipStream_t s) {
     if (sc.bvh_width == 4 && sc.trace_refill) {  // the production kernel, fed from a ray array
-        const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, rays, out};
+        const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, sc.trace_node_min, rays, out};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
         if (any)
             hipLaunchKernelGGL((k_trace4<kModeRays, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
@@ -1041,7 +1075,7 @@ void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
     if (w4 && sc.trace_refill) {
-        const TraceJob job{queue, queue_count, static_count, q.counts + 11, sc.trace_refill, nullptr, nullptr};
+        const TraceJob job{queue, queue_count, static_count, q.counts + 11, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
         if (stats)
             hipLaunchKernelGGL((k_trace4<kModeExtend, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
@@ -1070,7 +1104,7 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
     if (w4 && sc.trace_refill) {
-        const TraceJob job{nullptr, nullptr, 0u, q.counts + 12, sc.trace_refill, nullptr, nullptr};
+        const TraceJob job{nullptr, nullptr, 0u, q.counts + 12, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
         if (stats)
             hipLaunchKernelGGL((k_trace4<kModeShadow, true, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,

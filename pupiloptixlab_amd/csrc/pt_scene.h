@@ -128,6 +128,7 @@ struct DeviceScene {
     uint32_t bvh_width;   // 2 or 4: which node array the traversal kernels use
     uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
     uint32_t num_cus;       // compute units of the device (persistent grid size)
+    uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node
     const uint32_t *prim_inst;  // global prim id -> instance
     const DevInstance *instances;
     const DevMaterial *materials;

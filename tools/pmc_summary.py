@@ -41,6 +41,27 @@ def load(root):
     return vals, dur
 
 
+def traffic_json(root, kernel, out_path, note=""):
+    """Per-launch L2->fabric bytes of one kernel: 2 x FETCH_SIZE (gfx950 half-count
+    correction for 16 B/lane loads) + WRITE_SIZE, both KiB in rocprofv3."""
+    import json
+
+    vals, dur = load(root)
+    k = next(k for k in vals if k == kernel)
+    f = sum(vals[k]["FETCH_SIZE"]) / len(vals[k]["FETCH_SIZE"])
+    w = sum(vals[k]["WRITE_SIZE"]) / len(vals[k]["WRITE_SIZE"])
+    hit = sum(vals[k].get("TCC_HIT_sum", [0])) / max(1, len(vals[k].get("TCC_HIT_sum", [0])))
+    miss = sum(vals[k].get("TCC_MISS_sum", [0])) / max(1, len(vals[k].get("TCC_MISS_sum", [0])))
+    d = dur[k]
+    rec = {"kernel": k, "fetch_size_kib": f, "write_size_kib": w,
+           "traffic_bytes_per_launch": (2.0 * f + w) * 1024.0,
+           "l2_hit_rate": hit / max(1.0, hit + miss),
+           "avg_ms_under_pmc": sum(d) / len(d) / 1e6, "note": note}
+    with open(out_path, "w") as fh:
+        json.dump(rec, fh, indent=1)
+    print(json.dumps(rec))
+
+
 def main(root, filters):
     vals, dur = load(root)
     for k in sorted(vals, key=lambda k: -sum(dur[k])):
@@ -60,4 +81,7 @@ def main(root, filters):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2:])
+    if len(sys.argv) > 2 and sys.argv[2] == "--json":  # pmc_summary.py ROOT --json KERNEL OUT [NOTE]
+        traffic_json(sys.argv[1], sys.argv[3], sys.argv[4], " ".join(sys.argv[5:]))
+    else:
+        main(sys.argv[1], sys.argv[2:])
