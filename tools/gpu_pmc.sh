@@ -5,7 +5,7 @@ mkdir -p gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 rocprofv3 -L > $R/gpurun_out/pmc/counters.txt 2>&1 || true
-ARGS="--steps 1 --warmup 0 --cpu-baseline 0 ${BENCH_ARGS:-}"
+ARGS="--steps 2 --warmup 1 --cpu-baseline 0 ${BENCH_ARGS:-}"
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM SQ_INSTS_LDS" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" "SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"; do
   i=$((i+1))
