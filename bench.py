@@ -177,6 +177,7 @@ def main():
                        "rays_per_frame": rays_total / args.steps,
                        "path_samples_per_s": round(args.width * args.height * args.spp / (ms_per_step * 1e-3), 1),
                        "bvh_build_ms": round(st_bytes["build_ms"], 3),
+                       "bvh_nodes": int(st_bytes["bvh_nodes"]),
                        "avg_node_visits_per_ray": round(st_bytes["node_visits"] / max(1, rays_frame_local), 2),
                        "avg_prim_tests_per_ray": round(st_bytes["prim_tests"] / max(1, rays_frame_local), 2),
                        "stage_ms_per_frame": {"extend": round(ext_ms / args.steps, 3),

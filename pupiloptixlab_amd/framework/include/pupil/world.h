@@ -1,0 +1,63 @@
+// world.h — host scene of the C++ layer (framework/world/world.h:25-70 names).
+// Wraps the engine's pupil_world (XML loader, programmatic builder, emitter
+// table, camera matrices) and exposes the fields PTPass reads in the
+// reference: world->scene->sensor.film.{w,h}, world->scene->integrator.max_depth,
+// world->camera (CameraHelper, world/camera.h).
+#pragma once
+
+#include <filesystem>
+#include <memory>
+
+#include "framework.h"
+
+namespace Pupil::world {
+
+struct SceneInfo {
+    struct {
+        struct {
+            int w = 0, h = 0;
+        } film;
+    } sensor;
+    struct {
+        int max_depth = 1;
+    } integrator;
+};
+
+class CameraHelper {
+public:
+    const float *SampleToCamera() const noexcept { return m_s2c; }
+    const float *CameraToWorld() const noexcept { return m_c2w; }
+    // Replace the camera-to-world matrix (row-major 4x4) and fire
+    // EWorldEvent::CameraChange, like CameraHelper's setters (world/camera.cpp).
+    void SetCameraToWorld(const float c2w[16]) noexcept;
+    void Load(const pupil_scene_desc &d) noexcept;
+
+private:
+    float m_s2c[16] = {};
+    float m_c2w[16] = {};
+};
+
+class World {
+public:
+    std::unique_ptr<SceneInfo> scene;
+    std::unique_ptr<CameraHelper> camera;
+
+    World() noexcept;
+    ~World() noexcept;
+    World(const World &) = delete;
+    World &operator=(const World &) = delete;
+
+    bool LoadScene(const std::filesystem::path &xml) noexcept;
+    // Programmatic scenes: the caller filled `handle()` through pupil_world_*.
+    bool Finalize() noexcept;
+
+    pupil_world *handle() noexcept { return m_world; }
+    // Flattened scene for pupil_pt_create (valid until the world changes).
+    const pupil_scene_desc &Desc() const noexcept { return m_desc; }
+
+private:
+    pupil_world *m_world = nullptr;
+    pupil_scene_desc m_desc{};
+};
+
+}  // namespace Pupil::world

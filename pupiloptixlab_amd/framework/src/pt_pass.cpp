@@ -1,0 +1,119 @@
+// pt_pass.cpp — PTPass over the HIP engine (example/path_tracer/pt_pass.cpp).
+#include "pupil/pt_pass.h"
+
+#include <algorithm>
+
+namespace Pupil::pt {
+
+PTPass::PTPass(std::string_view name) noexcept : Pass(name) {
+    if (hipStreamCreateWithFlags(&m_stream, hipStreamNonBlocking) != hipSuccess) {
+        Log("%s: stream creation failed", this->name.c_str());
+        m_stream = nullptr;
+    }
+    BindingEventCallback();
+}
+
+PTPass::~PTPass() noexcept {
+    if (m_engine) pupil_pt_destroy(m_engine);
+    if (m_stream) (void)hipStreamDestroy(m_stream);
+}
+
+// pt_pass.cpp:39-57: refresh on dirty (camera, depth, accumulation reset),
+// one 1-spp frame, synchronise, advance seed and sample count.
+void PTPass::OnRun() noexcept {
+    if (!m_engine) return;
+    if (m_dirty) {
+        pupil_pt_set_camera(m_engine, m_world->camera->SampleToCamera(), m_world->camera->CameraToWorld());
+        m_frame_max_depth = (uint32_t)m_max_depth;
+        m_sample_cnt = 0;
+        m_random_seed = 0;
+        m_dirty = false;
+    }
+    pupil_pt_launch launch{};
+    launch.random_seed = m_random_seed;
+    launch.sample_cnt = m_sample_cnt;
+    launch.spp = 1;
+    launch.max_depth = m_frame_max_depth;
+    launch.accumulate = m_accumulated_flag ? 1u : 0u;
+    if (pupil_pt_render(m_engine, &m_frame, &launch, m_stream) != PUPIL_OK) {
+        Log("%s: render failed: %s", name.c_str(), pupil_last_error());
+        return;
+    }
+    (void)hipStreamSynchronize(m_stream);
+    m_sample_cnt += m_accumulated_flag ? 1u : 0u;
+    ++m_random_seed;
+}
+
+void PTPass::SetScene(world::World *world) noexcept {
+    if (!world) return;
+    m_world = world;
+    if (m_engine) {
+        pupil_pt_destroy(m_engine);
+        m_engine = nullptr;
+    }
+    const int w = world->scene->sensor.film.w, h = world->scene->sensor.film.h;
+    m_max_depth = world->scene->integrator.max_depth;
+    m_accumulated_flag = true;
+    auto *bm = BufferManager::instance();
+    Buffer *final_result = bm->GetBuffer(BufferManager::DEFAULT_FINAL_RESULT_BUFFER_NAME);
+    BufferDesc desc;
+    desc.width = (uint32_t)w;
+    desc.height = (uint32_t)h;
+    desc.name = "pt accum buffer";
+    desc.stride_in_byte = sizeof(float) * 4;
+    Buffer *accum = bm->AllocBuffer(desc);
+    desc.name = "albedo";
+    desc.flag = EBufferFlag::AllowDisplay;
+    desc.stride_in_byte = sizeof(float) * 3;
+    Buffer *albedo = bm->AllocBuffer(desc);
+    desc.name = "normal";
+    Buffer *normal = bm->AllocBuffer(desc);
+    desc.name = "test";
+    desc.stride_in_byte = sizeof(float);
+    Buffer *test = bm->AllocBuffer(desc);
+    if (!final_result || !accum || !albedo || !normal || !test) {
+        Log("%s: output buffers unavailable", name.c_str());
+        return;
+    }
+    m_frame = pupil_pt_frame{accum->cuda_ptr, final_result->cuda_ptr, albedo->cuda_ptr, normal->cuda_ptr,
+                             test->cuda_ptr, 0u, 0u};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (pupil_pt_create(&world->Desc(), dev, &m_engine) != PUPIL_OK) {
+        Log("%s: engine creation failed: %s", name.c_str(), pupil_last_error());
+        m_engine = nullptr;
+        return;
+    }
+    m_dirty = true;
+}
+
+void PTPass::SetMaxDepth(int depth) noexcept {
+    depth = std::clamp(depth, 1, 128);  // Inspector clamp, pt_pass.cpp:229
+    if (depth != m_max_depth) {
+        m_max_depth = depth;
+        m_dirty = true;
+    }
+}
+
+void PTPass::SetAccumulate(bool on) noexcept {
+    if (on != m_accumulated_flag) {
+        m_accumulated_flag = on;
+        m_dirty = true;
+    }
+}
+
+bool PTPass::Stats(pupil_pt_counters &out) noexcept { return m_engine && pupil_pt_stats(m_engine, &out) == PUPIL_OK; }
+
+void PTPass::BindingEventCallback() noexcept {
+    EventBinder<EWorldEvent::CameraChange>([this](void *) { m_dirty = true; });
+    EventBinder<EWorldEvent::RenderInstanceUpdate>([this](void *) { m_dirty = true; });
+    EventBinder<ESystemEvent::SceneLoad>([this](void *p) { SetScene(static_cast<world::World *>(p)); });
+}
+
+void PTPass::Inspector() noexcept {
+    Pass::Inspector();
+    Log("  sample count: %u, max trace depth: %d, accumulate radiance: %s", m_sample_cnt + 1, m_max_depth,
+        m_accumulated_flag ? "on" : "off");
+}
+
+}  // namespace Pupil::pt
