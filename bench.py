@@ -180,6 +180,14 @@ def main():
                        "bvh_nodes": int(st_bytes["bvh_nodes"]),
                        "avg_node_visits_per_ray": round(st_bytes["node_visits"] / max(1, rays_frame_local), 2),
                        "avg_prim_tests_per_ray": round(st_bytes["prim_tests"] / max(1, rays_frame_local), 2),
+                       "extend_rays_nodes_prims": [
+                           int(st_bytes["primary_rays"] + st_bytes["extension_rays"]),
+                           round(st_bytes["extend_node_visits"] / max(1, st_bytes["primary_rays"] + st_bytes["extension_rays"]), 2),
+                           round(st_bytes["extend_prim_tests"] / max(1, st_bytes["primary_rays"] + st_bytes["extension_rays"]), 2)],
+                       "shadow_rays_nodes_prims": [
+                           int(st_bytes["shadow_rays"]),
+                           round((st_bytes["node_visits"] - st_bytes["extend_node_visits"]) / max(1, st_bytes["shadow_rays"]), 2),
+                           round((st_bytes["prim_tests"] - st_bytes["extend_prim_tests"]) / max(1, st_bytes["shadow_rays"]), 2)],
                        "stage_ms_per_frame": {"extend": round(ext_ms / args.steps, 3),
                                               "shadow": round((trace_ms - ext_ms) / args.steps, 3),
                                               "shade": round(shade_ms / args.steps, 3)}},

@@ -124,12 +124,12 @@ struct pupil_pt {
         return e;
     }
     void release_state() {
-        void *bufs[] = {ps.ray_o, ps.ray_d, ps.hit, ps.thr, ps.rad, ps.misc, ps.sh_o, ps.sh_d, ps.sh_c, q.bins, q.next,
-                        q.shadow};
+        void *bufs[] = {ps.ray_o, ps.ray_d, ps.hit,  ps.thr,  ps.rad,    ps.misc, ps.sh_o,
+                        ps.sh_d, ps.sh_c, ps.mbin, ps.sflags, q.bins, q.nxsh, q.hist};
         for (void *b : bufs)
             if (b) (void)hipFree(b);
         ps = PathState{};
-        q.bins = q.next = q.shadow = nullptr;
+        q.bins = q.nxsh = q.hist = nullptr;
         cap = 0;
     }
     ~pupil_pt() {
@@ -245,9 +245,11 @@ int ensure_state(pupil_pt *pt, size_t paths) {
     HIP_TRY(hipMalloc((void **)&pt->ps.sh_o, sizeof(float4) * n));
     HIP_TRY(hipMalloc((void **)&pt->ps.sh_d, sizeof(float4) * n));
     HIP_TRY(hipMalloc((void **)&pt->ps.sh_c, sizeof(float4) * n));
-    HIP_TRY(hipMalloc((void **)&pt->q.bins, sizeof(uint32_t) * n * kNumQueues));
-    HIP_TRY(hipMalloc((void **)&pt->q.next, sizeof(uint32_t) * n));
-    HIP_TRY(hipMalloc((void **)&pt->q.shadow, sizeof(uint32_t) * n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.mbin, n));
+    HIP_TRY(hipMalloc((void **)&pt->ps.sflags, n));
+    HIP_TRY(hipMalloc((void **)&pt->q.bins, sizeof(uint32_t) * n));
+    HIP_TRY(hipMalloc((void **)&pt->q.nxsh, sizeof(uint32_t) * 2 * n));
+    HIP_TRY(hipMalloc((void **)&pt->q.hist, sizeof(uint32_t) * partition_hist_entries((uint32_t)n)));
     pt->q.capacity = (uint32_t)n;
     pt->cap = n;
     return PUPIL_OK;
@@ -456,7 +458,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     // traversal overflow stacks, counters, events
     pt->ovf_threads = trace_grid_blocks() * (uint32_t)kTraceBlock;
     if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 16) ||
-        pt->alloc(&pt->ray_log, 2 * 130) || pt->alloc(&pt->q.counts, 16))
+        pt->alloc(&pt->ray_log, 2 * 130) || pt->alloc(&pt->q.counts, kCountSlots))
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
@@ -559,27 +561,40 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     HIP_TRY(hipEventRecord(pt->ev_begin, s));
     if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 16 * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(pt->ray_log, 0, sizeof(uint32_t) * 2 * 130, s));
+    const uint32_t np = fp.num_paths;
+    Queues &q = pt->q;
+    // material bins of the traced paths -> q.bins (stable, increasing path id)
+    auto bin_paths = [&]() {
+        launch_partition(pt->ps.mbin, np, kPartMaxBins, false, q.bins, q.hist, q.counts, q.counts + kStartBins, s);
+    };
     launch_generate(pt->sc, fp, pt->ps, s);
-    HIP_TRY(hipMemsetAsync(pt->q.counts, 0, 16 * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(q.counts, 0, kCountSlots * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(pt->ps.mbin, 0xFF, np, s));
     ev0(0);
-    launch_extend(pt->sc, pt->ps, pt->q, nullptr, nullptr, fp.num_paths, pt->ovf, pt->ovf_threads, tsp, s);
+    launch_extend(pt->sc, pt->ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s);
     ev1();
+    bin_paths();
     for (uint32_t b = 0; b < bounces; b++) {
-        HIP_TRY(hipMemsetAsync(pt->q.counts + 9, 0, 4 * sizeof(uint32_t), s));  // next, shadow, 2 work counters
+        HIP_TRY(hipMemsetAsync(q.counts + kWorkExtend, 0, 3 * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(pt->ps.sflags, 0, np, s));
         ev0(2);
-        launch_shade(pt->sc, fp, pt->ps, pt->q, b, s);
+        launch_shade(pt->sc, fp, pt->ps, q, b, s);
         ev1();
-        if (b < 128)
-            HIP_TRY(hipMemcpyAsync(pt->ray_log + 2 * b, pt->q.counts + 9, 2 * sizeof(uint32_t),
-                                   hipMemcpyDeviceToDevice, s));
         if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
+            // next (bit 0) and shadow (bit 1) lists -> q.nxsh
+            launch_partition(pt->ps.sflags, np, 2, true, q.nxsh, q.hist, q.counts + kCntNext, q.counts + kStartNext,
+                             s);
+            if (b < 128)
+                HIP_TRY(hipMemcpyAsync(pt->ray_log + 2 * b, q.counts + kCntNext, 2 * sizeof(uint32_t),
+                                       hipMemcpyDeviceToDevice, s));
             ev0(1);
-            launch_shadow(pt->sc, pt->ps, pt->q, pt->ovf, pt->ovf_threads, tsp, s);
+            launch_shadow(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);
             ev1();
-            HIP_TRY(hipMemsetAsync(pt->q.counts, 0, 9 * sizeof(uint32_t), s));
+            HIP_TRY(hipMemsetAsync(pt->ps.mbin, 0xFF, np, s));
             ev0(0);
-            launch_extend(pt->sc, pt->ps, pt->q, pt->q.next, pt->q.counts + 9, 0u, pt->ovf, pt->ovf_threads, tsp, s);
+            launch_extend(pt->sc, pt->ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, tsp, s);
             ev1();
+            bin_paths();
         }
     }
     launch_accumulate(fp, pt->ps, s);
@@ -663,9 +678,9 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
     hipError_t e = hipMalloc((void **)&d_out, sizeof(float) * 4 * (size_t)n);
     if (e == hipSuccess) e = hipMemcpy(d_rays, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        e = hipMemsetAsync(pt->q.counts + 13, 0, sizeof(uint32_t), pt->own_stream);
+        e = hipMemsetAsync(pt->q.counts + kWorkRays, 0, sizeof(uint32_t), pt->own_stream);
         if (e == hipSuccess)
-            launch_trace_debug(pt->sc, d_rays, d_out, n, any_hit, pt->ovf, pt->ovf_threads, pt->q.counts + 13,
+            launch_trace_debug(pt->sc, d_rays, d_out, n, any_hit, pt->ovf, pt->ovf_threads, pt->q.counts + kWorkRays,
                                pt->own_stream);
         e = hipStreamSynchronize(pt->own_stream);
     }

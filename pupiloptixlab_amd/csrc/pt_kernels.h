@@ -28,13 +28,23 @@ struct PathState {
     float4 *sh_o;       // shadow ray origin, w = tmax
     float4 *sh_d;       // shadow ray direction
     float4 *sh_c;       // pending NEE contribution
+    uint8_t *mbin;      // extend -> material bin of the hit (0 miss, 1..7 EMatType, 8 unknown), 0xFF = not traced
+    uint8_t *sflags;    // shade -> bit 0: extension ray spawned, bit 1: shadow ray spawned
 };
 
+// Queues are rebuilt by a stable partition (queue_partition.hip) after each
+// stage, so every queue lists path ids in increasing order.
+constexpr int kPartMaxBins = 9;
+constexpr uint32_t kCntNext = 9, kCntShadow = 10;                      // counts[] slots
+constexpr uint32_t kWorkExtend = 11, kWorkShadow = 12, kWorkRays = 13;  // persistent-kernel work counters
+constexpr uint32_t kStartBins = 16, kStartNext = 25, kStartShadow = 26;
+constexpr uint32_t kCountSlots = 32;
+
 struct Queues {
-    uint32_t *bins;      // kNumQueues * capacity
-    uint32_t *next;      // capacity
-    uint32_t *shadow;    // capacity
-    uint32_t *counts;    // [0..8] bins, [9] next, [10] shadow
+    uint32_t *bins;      // capacity: material bin b occupies [counts[kStartBins + b], + counts[b])
+    uint32_t *nxsh;      // 2 * capacity: next ids from counts[kStartNext], shadow ids from counts[kStartShadow]
+    uint32_t *counts;    // kCountSlots entries, see above
+    uint32_t *hist;      // partition scratch, partition_hist_entries(capacity)
     uint32_t capacity;
 };
 
@@ -74,6 +84,11 @@ uint32_t trace_grid_blocks();
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
                         uint32_t ovf_threads, uint32_t *work, hipStream_t s);
 void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, hipStream_t s);
+
+// stable partition of path ids 0..n-1 by a key byte (queue_partition.hip)
+uint32_t partition_hist_entries(uint32_t n);
+void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, bool flags, uint32_t *out, uint32_t *hist,
+                      uint32_t *counts_out, uint32_t *starts_out, hipStream_t s);
 
 // LBVH builder (bvh_build.hip)
 struct BvhBuildInput {

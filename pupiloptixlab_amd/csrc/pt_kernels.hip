@@ -28,17 +28,6 @@ namespace {
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
-// Wave-aggregated append: one atomic per wave per queue (wave-ballot prefix sum).
-__device__ __forceinline__ void wave_append(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
-    const unsigned long long m = __ballot(pred);
-    if (m == 0ull) return;
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if ((int)lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (pred) queue[base + (uint32_t)__popcll(m & lanemask_lt())] = value;
-}
-
 __device__ __forceinline__ vec3 f3(float4 v) { return v3(v.x, v.y, v.z); }
 __device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
@@ -322,7 +311,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend(DeviceScene sc, PathStat
     st.ovf_stride = ovf_threads;
     uint32_t nv = 0, pt = 0;
     const uint32_t stride = gridDim.x * blockDim.x;
-    // whole waves iterate together so wave_append sees every lane
     const uint32_t wave_base = (blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
     for (uint32_t base = wave_base; base < count; base += stride) {
         const uint32_t i = base + lane_id();
@@ -343,16 +331,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend(DeviceScene sc, PathStat
                 const uint32_t mt = __float_as_uint(sc.prims[3 * best_idx + 2].w);
                 bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
             }
-        }
-        // bin by material: loop over the distinct bins present in the wave
-        bool pending = valid;
-        while (__any(pending)) {
-            const unsigned long long m = __ballot(pending);
-            const int leader = __ffsll((long long)m) - 1;
-            const uint32_t b = __shfl(bin, leader);
-            const bool mine = pending && bin == b;
-            wave_append(mine, p, q.bins + (size_t)b * q.capacity, q.counts + b);
-            if (mine) pending = false;
+            ps.mbin[p] = (uint8_t)bin;  // material bin for the partition
         }
     }
     flush_stats<STATS>(&stats, nv, pt);
@@ -363,7 +342,8 @@ template <bool STATS, int W>
 __global__ __launch_bounds__(kTraceBlock) void k_shadow(DeviceScene sc, PathState ps, Queues q, int *ovf,
                                                         uint32_t ovf_threads, TraceStats stats) {
     __shared__ int s_stack[kStackLds * kTraceBlock];
-    const uint32_t count = q.counts[10];
+    const uint32_t count = q.counts[kCntShadow];
+    const uint32_t *shadow_q = q.nxsh + q.counts[kStartShadow];
     Stack st;
     st.lds = s_stack + threadIdx.x;
     const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -372,7 +352,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow(DeviceScene sc, PathStat
     uint32_t nv = 0, pt = 0;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = gtid; i < count; i += stride) {
-        const uint32_t p = q.shadow[i];
+        const uint32_t p = shadow_q[i];
         const float4 o = ps.sh_o[p];
         const float4 d = ps.sh_d[p];
         const RayPre r = ray_pre(f3(o), f3(d));
@@ -506,7 +486,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                                                         int *ovf, uint32_t ovf_threads, TraceStats stats) {
     constexpr float kInf = __builtin_huge_valf();
     __shared__ int s_ring[kRing * kTraceBlock];
-    const uint32_t count = MODE == kModeShadow ? q.counts[10] : (job.count_ptr ? *job.count_ptr : job.static_count);
+    const uint32_t count =
+        MODE == kModeShadow ? q.counts[kCntShadow] : (job.count_ptr ? *job.count_ptr : job.static_count);
+    const uint32_t *shadow_q = MODE == kModeShadow ? q.nxsh + q.counts[kStartShadow] : nullptr;
     RingStack st;
     st.lds = s_ring + threadIdx.x;
     st.ovf = ovf + blockIdx.x * blockDim.x + threadIdx.x;
@@ -547,7 +529,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                         tmin = 0.001f;
                         tmax = kMaxDistance;
                     } else if (MODE == kModeShadow) {
-                        p = q.shadow[i];
+                        p = shadow_q[i];
                         o = ps.sh_o[p];
                         d = ps.sh_d[p];
                         tmin = 0.001f;
@@ -635,15 +617,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                     const uint32_t mt = __float_as_uint(sc.prims[3 * best_idx + 2].w);
                     bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
                 }
-            }
-            bool pending = done;
-            while (__any(pending)) {
-                const unsigned long long m = __ballot(pending);
-                const int leader = __ffsll((long long)m) - 1;
-                const uint32_t b = __shfl(bin, leader);
-                const bool mine = pending && bin == b;
-                wave_append(mine, p, q.bins + (size_t)b * q.capacity, q.counts + b);
-                if (mine) pending = false;
+                ps.mbin[p] = (uint8_t)bin;  // material bin for the partition
             }
         } else if (MODE == kModeShadow) {
             if (done && !found) {  // main.cu:124-139
@@ -795,7 +769,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DeviceScene sc, FramePara
                                                        uint32_t bounce) {
     const uint32_t bin = MAT == 0u ? 8u : MAT;
     const uint32_t count = q.counts[bin];
-    const uint32_t *queue = q.bins + (size_t)bin * q.capacity;
+    const uint32_t *queue = q.bins + q.counts[kStartBins + bin];
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t wave_base = (blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
     for (uint32_t base = wave_base; base < count; base += stride) {
@@ -922,8 +896,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DeviceScene sc, FramePara
             ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 8), __float_as_uint(geo.texcoord.x),
                                     __float_as_uint(geo.texcoord.y));
         }
-        wave_append(push_shadow, p, q.shadow, q.counts + 10);
-        wave_append(push_next, p, q.next, q.counts + 9);
+        if (valid) ps.sflags[p] = (uint8_t)((push_next ? 1u : 0u) | (push_shadow ? 2u : 0u));
     }
 }
 
@@ -1075,7 +1048,7 @@ void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
     if (w4 && sc.trace_refill) {
-        const TraceJob job{queue, queue_count, static_count, q.counts + 11, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
+        const TraceJob job{queue, queue_count, static_count, q.counts + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
         if (stats)
             hipLaunchKernelGGL((k_trace4<kModeExtend, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
@@ -1104,7 +1077,7 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
     if (w4 && sc.trace_refill) {
-        const TraceJob job{nullptr, nullptr, 0u, q.counts + 12, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
+        const TraceJob job{nullptr, nullptr, 0u, q.counts + kWorkShadow, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
         if (stats)
             hipLaunchKernelGGL((k_trace4<kModeShadow, true, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,

@@ -1,0 +1,161 @@
+// queue_partition.hip — stable partition of path ids by a per-path key byte.
+//
+// The wavefront stages no longer append path ids to queues with atomics (which
+// leaves every queue in completion order, so the next stage gathers its 16-B
+// path-state records from random addresses).  Instead each stage writes one
+// key byte per path (extend: material bin; shade: next/shadow flags) and this
+// partition lists the ids of every bin in increasing path order, so the next
+// stage reads and writes path state in runs of consecutive records.
+//
+//   k_part_count    per block tile of 16384 paths: count of each bin (wave ballots)
+//   k_part_scan     one block: exclusive scan of the bin-major histogram,
+//                   per-bin start and count
+//   k_part_scatter  per tile: recount per wave, then rank with ballots and write
+//
+// Exclusive mode: key k puts the path in bin k (0xFF = in no bin).
+// Flag mode: bit b of the key puts the path in bin b (a path can be in several).
+#include "pt_kernels.h"
+
+namespace pupil {
+
+namespace {
+
+constexpr int kPartBlock = 256;               // 4 waves
+constexpr int kPartRounds = 64;               // rounds of 64 paths per wave
+constexpr uint32_t kPartWaveItems = 64u * kPartRounds;
+constexpr uint32_t kPartTile = 4u * kPartWaveItems;
+
+template <bool FLAGS>
+__device__ __forceinline__ bool in_bin(uint32_t k, uint32_t b) {
+    return FLAGS ? ((k >> b) & 1u) != 0u : k == b;
+}
+
+__device__ __forceinline__ unsigned long long lanes_below() { return (1ull << __lane_id()) - 1ull; }
+
+template <bool FLAGS>
+__device__ __forceinline__ void count_wave(const uint8_t *keys, uint32_t n, uint32_t nbins, uint32_t base,
+                                           uint32_t cnt[kPartMaxBins]) {
+#pragma unroll
+    for (int b = 0; b < kPartMaxBins; b++) cnt[b] = 0;
+    for (int r = 0; r < kPartRounds; r++) {
+        const uint32_t i = base + (uint32_t)r * 64u + __lane_id();
+        const uint32_t k = i < n ? keys[i] : (FLAGS ? 0u : 0xFFu);
+#pragma unroll
+        for (int b = 0; b < kPartMaxBins; b++)
+            if ((uint32_t)b < nbins) cnt[b] += (uint32_t)__popcll(__ballot(in_bin<FLAGS>(k, (uint32_t)b)));
+    }
+}
+
+template <bool FLAGS>
+__global__ __launch_bounds__(kPartBlock) void k_part_count(const uint8_t *keys, uint32_t n, uint32_t nbins,
+                                                           uint32_t *hist, uint32_t nblk) {
+    __shared__ uint32_t s[4][kPartMaxBins];
+    const uint32_t wave = threadIdx.x >> 6;
+    uint32_t cnt[kPartMaxBins];
+    count_wave<FLAGS>(keys, n, nbins, blockIdx.x * kPartTile + wave * kPartWaveItems, cnt);
+    if (__lane_id() == 0)
+        for (int b = 0; b < kPartMaxBins; b++) s[wave][b] = cnt[b];
+    __syncthreads();
+    const uint32_t t = threadIdx.x;
+    if (t < nbins) hist[t * nblk + blockIdx.x] = s[0][t] + s[1][t] + s[2][t] + s[3][t];
+}
+
+// Exclusive scan of m = nbins * nblk entries in one block of 1024 threads.
+__global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nblk, uint32_t nbins,
+                                                    uint32_t *counts_out, uint32_t *starts_out) {
+    __shared__ uint32_t wave_sum[16];
+    __shared__ uint32_t total;
+    const uint32_t m = nbins * nblk;
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (m + 1023u) / 1024u;
+    const uint32_t beg = min(t * per, m), end = min(beg + per, m);
+    uint32_t sum = 0;
+    for (uint32_t i = beg; i < end; i++) sum += hist[i];
+    // inclusive wave scan
+    uint32_t inc = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(inc, o);
+        if ((int)__lane_id() >= o) inc += v;
+    }
+    if (__lane_id() == 63) wave_sum[t >> 6] = inc;
+    __syncthreads();
+    if (t < 64) {
+        uint32_t w = t < 16 ? wave_sum[t] : 0u;
+        uint32_t winc = w;
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t v = __shfl_up(winc, o);
+            if ((int)t >= o) winc += v;
+        }
+        if (t < 16) wave_sum[t] = winc - w;  // exclusive wave offsets
+        if (t == 15) total = winc;
+    }
+    __syncthreads();
+    uint32_t run = wave_sum[t >> 6] + inc - sum;
+    for (uint32_t i = beg; i < end; i++) {
+        const uint32_t v = hist[i];
+        hist[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    if (t < nbins) {
+        const uint32_t start = hist[t * nblk];
+        const uint32_t next = t + 1 < nbins ? hist[(t + 1) * nblk] : total;
+        starts_out[t] = start;
+        counts_out[t] = next - start;
+    }
+}
+
+template <bool FLAGS>
+__global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys, uint32_t n, uint32_t nbins,
+                                                             const uint32_t *hist, uint32_t nblk, uint32_t *out) {
+    __shared__ uint32_t s[4][kPartMaxBins];
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t base = blockIdx.x * kPartTile + wave * kPartWaveItems;
+    uint32_t off[kPartMaxBins];
+    count_wave<FLAGS>(keys, n, nbins, base, off);
+    if (__lane_id() == 0)
+        for (int b = 0; b < kPartMaxBins; b++) s[wave][b] = off[b];
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < kPartMaxBins; b++) {
+        if ((uint32_t)b >= nbins) continue;
+        uint32_t o = hist[b * nblk + blockIdx.x];
+        for (uint32_t w = 0; w < wave; w++) o += s[w][b];
+        off[b] = o;
+    }
+    for (int r = 0; r < kPartRounds; r++) {
+        const uint32_t i = base + (uint32_t)r * 64u + __lane_id();
+        const uint32_t k = i < n ? keys[i] : (FLAGS ? 0u : 0xFFu);
+#pragma unroll
+        for (int b = 0; b < kPartMaxBins; b++) {
+            if ((uint32_t)b >= nbins) continue;
+            const bool mine = in_bin<FLAGS>(k, (uint32_t)b);
+            const unsigned long long m = __ballot(mine);
+            if (mine) out[off[b] + (uint32_t)__popcll(m & lanes_below())] = i;
+            off[b] += (uint32_t)__popcll(m);
+        }
+    }
+}
+
+}  // namespace
+
+uint32_t partition_hist_entries(uint32_t n) { return kPartMaxBins * ((n + kPartTile - 1) / kPartTile); }
+
+void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, bool flags, uint32_t *out, uint32_t *hist,
+                      uint32_t *counts_out, uint32_t *starts_out, hipStream_t s) {
+    const uint32_t nblk = (n + kPartTile - 1) / kPartTile;
+    if (nblk == 0) {
+        (void)hipMemsetAsync(counts_out, 0, sizeof(uint32_t) * nbins, s);
+        (void)hipMemsetAsync(starts_out, 0, sizeof(uint32_t) * nbins, s);
+        return;
+    }
+    if (flags) hipLaunchKernelGGL(k_part_count<true>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, hist, nblk);
+    else hipLaunchKernelGGL(k_part_count<false>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, hist, nblk);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, hist, nblk, nbins, counts_out, starts_out);
+    if (flags)
+        hipLaunchKernelGGL(k_part_scatter<true>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, hist, nblk, out);
+    else
+        hipLaunchKernelGGL(k_part_scatter<false>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, hist, nblk, out);
+}
+
+}  // namespace pupil
