@@ -565,7 +565,8 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     Queues &q = pt->q;
     // material bins of the traced paths -> q.bins (stable, increasing path id)
     auto bin_paths = [&]() {
-        launch_partition(pt->ps.mbin, np, kPartMaxBins, false, q.bins, q.hist, q.counts, q.counts + kStartBins, s);
+        launch_partition(pt->ps.mbin, np, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
+                         q.counts + kStartBins, q.counts + kScratch, s);
     };
     launch_generate(pt->sc, fp, pt->ps, s);
     HIP_TRY(hipMemsetAsync(q.counts, 0, kCountSlots * sizeof(uint32_t), s));
@@ -581,9 +582,10 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
         launch_shade(pt->sc, fp, pt->ps, q, b, s);
         ev1();
         if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
-            // next (bit 0) and shadow (bit 1) lists -> q.nxsh
-            launch_partition(pt->ps.sflags, np, 2, true, q.nxsh, q.hist, q.counts + kCntNext, q.counts + kStartNext,
-                             s);
+            // next (bit 0) and shadow (bit 1) lists -> q.nxsh, each in increasing path order
+            // (grouping the next list by direction octant measured slower: 21.2 vs 20.8 ms extend)
+            launch_partition(pt->ps.sflags, np, 2, kPartFlags, 0u, q.nxsh, q.hist, q.counts + kCntNext,
+                             q.counts + kStartNext, nullptr, s);
             if (b < 128)
                 HIP_TRY(hipMemcpyAsync(pt->ray_log + 2 * b, q.counts + kCntNext, 2 * sizeof(uint32_t),
                                        hipMemcpyDeviceToDevice, s));

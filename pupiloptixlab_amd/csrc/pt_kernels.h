@@ -35,17 +35,26 @@ struct PathState {
 // Queues are rebuilt by a stable partition (queue_partition.hip) after each
 // stage, so every queue lists path ids in increasing order.
 constexpr int kPartMaxBins = 9;
-constexpr uint32_t kCntNext = 9, kCntShadow = 10;                      // counts[] slots
+// counts[] slots
+constexpr uint32_t kCntNext = 9, kCntShadow = 10;                      // queue lengths
 constexpr uint32_t kWorkExtend = 11, kWorkShadow = 12, kWorkRays = 13;  // persistent-kernel work counters
-constexpr uint32_t kStartBins = 16, kStartNext = 25, kStartShadow = 26;
+constexpr uint32_t kStartBins = 16;                                    // [16..24] material bin starts
+constexpr uint32_t kStartNext = 25, kStartShadow = 26;                 // next / shadow regions of nxsh
+constexpr uint32_t kScratch = 27;
 constexpr uint32_t kCountSlots = 32;
 
 struct Queues {
     uint32_t *bins;      // capacity: material bin b occupies [counts[kStartBins + b], + counts[b])
-    uint32_t *nxsh;      // 2 * capacity: next ids from counts[kStartNext], shadow ids from counts[kStartShadow]
+    uint32_t *nxsh;      // 2 * capacity: next ids from counts[kStartNext] (= 0), shadow ids from counts[kStartShadow]
     uint32_t *counts;    // kCountSlots entries, see above
     uint32_t *hist;      // partition scratch, partition_hist_entries(capacity)
     uint32_t capacity;
+};
+
+// partition key modes (queue_partition.hip)
+enum PartMode : int {
+    kPartExclusive = 0,  // bin = key >> shift (0xFF = none)
+    kPartFlags = 1,      // bin b <=> bit (shift + b) of the key
 };
 
 struct FrameParams {
@@ -67,7 +76,7 @@ struct FrameParams {
 };
 
 struct TraceStats {
-    unsigned long long *counters;  // [0] nodes, [1] prims
+    unsigned long long *counters;  // [0..1] closest-hit nodes/prims, [14..15] shadow, [2..13] diagnostics
 };
 
 // wavefront stages
@@ -87,8 +96,8 @@ void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, 
 
 // stable partition of path ids 0..n-1 by a key byte (queue_partition.hip)
 uint32_t partition_hist_entries(uint32_t n);
-void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, bool flags, uint32_t *out, uint32_t *hist,
-                      uint32_t *counts_out, uint32_t *starts_out, hipStream_t s);
+void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
+                      uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, hipStream_t s);
 
 // LBVH builder (bvh_build.hip)
 struct BvhBuildInput {

@@ -12,8 +12,8 @@
 //                   per-bin start and count
 //   k_part_scatter  per tile: recount per wave, then rank with ballots and write
 //
-// Exclusive mode: key k puts the path in bin k (0xFF = in no bin).
-// Flag mode: bit b of the key puts the path in bin b (a path can be in several).
+// Modes (PartMode, pt_kernels.h): exclusive (bin = key >> shift, 0xFF none),
+// flags (bit shift + b puts the path in bin b; a path can be in several).
 #include "pt_kernels.h"
 
 namespace pupil {
@@ -25,34 +25,41 @@ constexpr int kPartRounds = 64;               // rounds of 64 paths per wave
 constexpr uint32_t kPartWaveItems = 64u * kPartRounds;
 constexpr uint32_t kPartTile = 4u * kPartWaveItems;
 
-template <bool FLAGS>
-__device__ __forceinline__ bool in_bin(uint32_t k, uint32_t b) {
-    return FLAGS ? ((k >> b) & 1u) != 0u : k == b;
+// key value that is in no bin
+template <int MODE>
+__device__ __forceinline__ uint32_t no_key() {
+    return MODE == kPartExclusive ? 0xFFu : 0u;
+}
+
+template <int MODE>
+__device__ __forceinline__ bool in_bin(uint32_t k, uint32_t b, uint32_t shift) {
+    if (MODE == kPartExclusive) return (k >> shift) == b && k != 0xFFu;
+    return ((k >> (shift + b)) & 1u) != 0u;  // kPartFlags
 }
 
 __device__ __forceinline__ unsigned long long lanes_below() { return (1ull << __lane_id()) - 1ull; }
 
-template <bool FLAGS>
-__device__ __forceinline__ void count_wave(const uint8_t *keys, uint32_t n, uint32_t nbins, uint32_t base,
-                                           uint32_t cnt[kPartMaxBins]) {
+template <int MODE>
+__device__ __forceinline__ void count_wave(const uint8_t *keys, uint32_t n, uint32_t nbins, uint32_t shift,
+                                           uint32_t base, uint32_t cnt[kPartMaxBins]) {
 #pragma unroll
     for (int b = 0; b < kPartMaxBins; b++) cnt[b] = 0;
     for (int r = 0; r < kPartRounds; r++) {
         const uint32_t i = base + (uint32_t)r * 64u + __lane_id();
-        const uint32_t k = i < n ? keys[i] : (FLAGS ? 0u : 0xFFu);
+        const uint32_t k = i < n ? keys[i] : no_key<MODE>();
 #pragma unroll
         for (int b = 0; b < kPartMaxBins; b++)
-            if ((uint32_t)b < nbins) cnt[b] += (uint32_t)__popcll(__ballot(in_bin<FLAGS>(k, (uint32_t)b)));
+            if ((uint32_t)b < nbins) cnt[b] += (uint32_t)__popcll(__ballot(in_bin<MODE>(k, (uint32_t)b, shift)));
     }
 }
 
-template <bool FLAGS>
+template <int MODE>
 __global__ __launch_bounds__(kPartBlock) void k_part_count(const uint8_t *keys, uint32_t n, uint32_t nbins,
-                                                           uint32_t *hist, uint32_t nblk) {
+                                                           uint32_t shift, uint32_t *hist, uint32_t nblk) {
     __shared__ uint32_t s[4][kPartMaxBins];
     const uint32_t wave = threadIdx.x >> 6;
     uint32_t cnt[kPartMaxBins];
-    count_wave<FLAGS>(keys, n, nbins, blockIdx.x * kPartTile + wave * kPartWaveItems, cnt);
+    count_wave<MODE>(keys, n, nbins, shift, blockIdx.x * kPartTile + wave * kPartWaveItems, cnt);
     if (__lane_id() == 0)
         for (int b = 0; b < kPartMaxBins; b++) s[wave][b] = cnt[b];
     __syncthreads();
@@ -62,7 +69,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part_count(const uint8_t *keys, 
 
 // Exclusive scan of m = nbins * nblk entries in one block of 1024 threads.
 __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nblk, uint32_t nbins,
-                                                    uint32_t *counts_out, uint32_t *starts_out) {
+                                                    uint32_t *counts_out, uint32_t *starts_out,
+                                                    uint32_t *total_out) {
     __shared__ uint32_t wave_sum[16];
     __shared__ uint32_t total;
     const uint32_t m = nbins * nblk;
@@ -103,16 +111,18 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nbl
         starts_out[t] = start;
         counts_out[t] = next - start;
     }
+    if (t == 0 && total_out) *total_out = total;
 }
 
-template <bool FLAGS>
+template <int MODE>
 __global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys, uint32_t n, uint32_t nbins,
-                                                             const uint32_t *hist, uint32_t nblk, uint32_t *out) {
+                                                             uint32_t shift, const uint32_t *hist, uint32_t nblk,
+                                                             uint32_t *out) {
     __shared__ uint32_t s[4][kPartMaxBins];
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * kPartTile + wave * kPartWaveItems;
     uint32_t off[kPartMaxBins];
-    count_wave<FLAGS>(keys, n, nbins, base, off);
+    count_wave<MODE>(keys, n, nbins, shift, base, off);
     if (__lane_id() == 0)
         for (int b = 0; b < kPartMaxBins; b++) s[wave][b] = off[b];
     __syncthreads();
@@ -125,11 +135,11 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys
     }
     for (int r = 0; r < kPartRounds; r++) {
         const uint32_t i = base + (uint32_t)r * 64u + __lane_id();
-        const uint32_t k = i < n ? keys[i] : (FLAGS ? 0u : 0xFFu);
+        const uint32_t k = i < n ? keys[i] : no_key<MODE>();
 #pragma unroll
         for (int b = 0; b < kPartMaxBins; b++) {
             if ((uint32_t)b >= nbins) continue;
-            const bool mine = in_bin<FLAGS>(k, (uint32_t)b);
+            const bool mine = in_bin<MODE>(k, (uint32_t)b, shift);
             const unsigned long long m = __ballot(mine);
             if (mine) out[off[b] + (uint32_t)__popcll(m & lanes_below())] = i;
             off[b] += (uint32_t)__popcll(m);
@@ -141,21 +151,25 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys
 
 uint32_t partition_hist_entries(uint32_t n) { return kPartMaxBins * ((n + kPartTile - 1) / kPartTile); }
 
-void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, bool flags, uint32_t *out, uint32_t *hist,
-                      uint32_t *counts_out, uint32_t *starts_out, hipStream_t s) {
+void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
+                      uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, hipStream_t s) {
     const uint32_t nblk = (n + kPartTile - 1) / kPartTile;
     if (nblk == 0) {
         (void)hipMemsetAsync(counts_out, 0, sizeof(uint32_t) * nbins, s);
         (void)hipMemsetAsync(starts_out, 0, sizeof(uint32_t) * nbins, s);
+        if (total_out) (void)hipMemsetAsync(total_out, 0, sizeof(uint32_t), s);
         return;
     }
-    if (flags) hipLaunchKernelGGL(k_part_count<true>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, hist, nblk);
-    else hipLaunchKernelGGL(k_part_count<false>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, hist, nblk);
-    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, hist, nblk, nbins, counts_out, starts_out);
-    if (flags)
-        hipLaunchKernelGGL(k_part_scatter<true>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, hist, nblk, out);
-    else
-        hipLaunchKernelGGL(k_part_scatter<false>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, hist, nblk, out);
+#define PART_RUN(M)                                                                                                \
+    hipLaunchKernelGGL(k_part_count<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk);    \
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, hist, nblk, nbins, counts_out, starts_out,          \
+                       total_out);                                                                                 \
+    hipLaunchKernelGGL(k_part_scatter<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk, out)
+    switch (mode) {
+    case kPartExclusive: PART_RUN(kPartExclusive); break;
+    case kPartFlags: PART_RUN(kPartFlags); break;
+    }
+#undef PART_RUN
 }
 
 }  // namespace pupil
