@@ -443,10 +443,48 @@ struct TraceJob {
     float *out;                 // kModeRays: 4 floats per ray
 };
 
-// One node of the quantized BVH4: child boxes decoded exactly as the builder
-// verified them (origin + q * 2^e; the product is exact, so the fma rounds
-// once like the builder's sum), near/far planes picked by the ray's direction
-// signs (equal to the min/max of the two slabs), conservative far distance.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pk2(float a, float b) {
+    pf2 v;
+    v.x = a;
+    v.y = b;
+    return v;
+}
+__device__ __forceinline__ pf2 splat(float a) { return pk2(a, a); }
+__device__ __forceinline__ pf2 pfma(pf2 a, pf2 b, pf2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ float ubyte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xFFu); }
+
+// One node of the quantized BVH4.  Child plane k on an axis is
+// P = o_node + q_k * s (s a power of two, so q_k * s is exact; the builder
+// verified that fl(P) bounds the child box).  The slab distance is evaluated as
+//     t = fma(q_k, s * idir, (o_node - o_ray) * idir -/+ E)
+// i.e. one fma per plane, with per-node terms shared by the four children.  E
+// bounds every rounding against the exact (fl(P) - o_ray) / d:
+//   |o_node - o_ray| |idir| 5.03u  (subtraction, product, fma, idir rounding)
+// + |o_node| |idir| 1.01u          (fl(P) vs P)
+// + 765 s |idir| 1.01u             (fma rounding of the q*s*idir part, idir rounding)
+// + 1.01u E;  E = (|o_node - o_ray| + |o_node| + 512 s) |idir| 2^-21 covers it
+// (2^-21 = 8u) even after its own rounding.  Near planes are lowered and far
+// planes raised by E, so the test is conservative: a box containing a
+// primitive the exact test would report is never culled, and closest hits stay
+// independent of the BVH.  Overflow (huge idir) gives +-inf/NaN planes, which
+// fmaxf/fminf ignore (IEEE maxNum), i.e. no culling on that axis.
+struct AxisTerms {
+    float b;       // s * idir (exact)
+    float an, af;  // (o_node - o_ray) * idir - E, + E
+};
+
+__device__ __forceinline__ AxisTerms axis_terms(float onode, float s, float oray, float idir) {
+    AxisTerms t;
+    const float A = onode - oray;
+    const float a = A * idir;
+    const float e = __builtin_fmaf(512.f, s, fabsf(A) + fabsf(onode)) * (fabsf(idir) * 0x1p-21f);
+    t.b = s * idir;
+    t.an = a - e;
+    t.af = a + e;
+    return t;
+}
+
 __device__ __forceinline__ void visit4(const Bvh4Node &n, const RayPre &r, float tmin, float tmax, float t[4],
                                        int l[4]) {
     constexpr float kInf = __builtin_huge_valf();
@@ -457,20 +495,17 @@ __device__ __forceinline__ void visit4(const Bvh4Node &n, const RayPre &r, float
     const uint32_t nx = px ? n.qlo_x : n.qhi_x, fx = px ? n.qhi_x : n.qlo_x;
     const uint32_t ny = py ? n.qlo_y : n.qhi_y, fy = py ? n.qhi_y : n.qlo_y;
     const uint32_t nz = pz ? n.qlo_z : n.qhi_z, fz = pz ? n.qhi_z : n.qlo_z;
+    const AxisTerms X = axis_terms(n.ox, sx, r.o.x, r.idir.x);
+    const AxisTerms Y = axis_terms(n.oy, sy, r.o.y, r.idir.y);
+    const AxisTerms Z = axis_terms(n.oz, sz, r.o.z, r.idir.z);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const float bnx = __builtin_fmaf((float)((nx >> (8 * k)) & 0xFFu), sx, n.ox);
-        const float bfx = __builtin_fmaf((float)((fx >> (8 * k)) & 0xFFu), sx, n.ox);
-        const float bny = __builtin_fmaf((float)((ny >> (8 * k)) & 0xFFu), sy, n.oy);
-        const float bfy = __builtin_fmaf((float)((fy >> (8 * k)) & 0xFFu), sy, n.oy);
-        const float bnz = __builtin_fmaf((float)((nz >> (8 * k)) & 0xFFu), sz, n.oz);
-        const float bfz = __builtin_fmaf((float)((fz >> (8 * k)) & 0xFFu), sz, n.oz);
-        const float tn = fmaxf(fmaxf(fmaxf((bnx - r.o.x) * r.idir.x, (bny - r.o.y) * r.idir.y),
-                                     (bnz - r.o.z) * r.idir.z),
+        const float tn = fmaxf(fmaxf(fmaxf(__builtin_fmaf(ubyte(nx, k), X.b, X.an), __builtin_fmaf(ubyte(ny, k), Y.b, Y.an)),
+                                     __builtin_fmaf(ubyte(nz, k), Z.b, Z.an)),
                                tmin);
-        float tf = fminf(fminf(fminf((bfx - r.o.x) * r.idir.x, (bfy - r.o.y) * r.idir.y), (bfz - r.o.z) * r.idir.z),
-                         tmax);
-        tf = tf * kBoxConservative;
+        const float tf = fminf(fminf(fminf(__builtin_fmaf(ubyte(fx, k), X.b, X.af), __builtin_fmaf(ubyte(fy, k), Y.b, Y.af)),
+                                     __builtin_fmaf(ubyte(fz, k), Z.b, Z.af)),
+                               tmax);
         l[k] = n.child[k];
         t[k] = (tn <= tf && l[k] != kEmptyLink) ? tn : kInf;
     }
