@@ -36,17 +36,31 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--spheres", type=int, default=500, help="500 -> 1,000,004 triangles (config 4)")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=8)
-    ap.add_argument("--max-depth", type=int, default=4)
+    ap.add_argument("--config", type=int, default=4, choices=(3, 4, 5),
+                    help="BASELINE.json configs[k-1]: 3 = 250k-tri field, 4 = 1M-tri field (headline), "
+                         "5 = 40 x 250k-tri instanced rough dielectric/plastic field, 3840x2160 16 spp D6")
+    ap.add_argument("--spheres", type=int, default=None, help="spheres in the field (configs 3/4) or per BLAS (5)")
+    ap.add_argument("--instances", type=int, default=40, help="config 5 instances")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--max-depth", type=int, default=None)
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1 only)")
-    ap.add_argument("--cpu-sample-stride", type=int, default=1, help="CPU baseline renders every k-th pixel")
+    ap.add_argument("--cpu-sample-stride", type=int, default=None,
+                    help="CPU baseline renders every k-th pixel (default: full frame for configs 3/4, 1/16 for 5)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--save", default="", help="write the frame as PNG (rank 0)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    defaults = {3: (125, 1920, 1080, 8, 4, 1), 4: (500, 1920, 1080, 8, 4, 1), 5: (125, 3840, 2160, 16, 6, 16)}
+    sph, w, h, spp, depth, stride = defaults[args.config]
+    args.spheres = sph if args.spheres is None else args.spheres
+    args.width = w if args.width is None else args.width
+    args.height = h if args.height is None else args.height
+    args.spp = spp if args.spp is None else args.spp
+    args.max_depth = depth if args.max_depth is None else args.max_depth
+    args.cpu_sample_stride = stride if args.cpu_sample_stride is None else args.cpu_sample_stride
+    return args
 
 
 def main():
@@ -65,13 +79,17 @@ def main():
     from pupiloptixlab_amd import scenes
     from pupiloptixlab_amd.pt_pass import PTPass, FINAL_RESULT
 
-    scene = scenes.sphere_field(args.spheres, args.width, args.height, args.max_depth, seed=1)
+    if args.config == 5:
+        scene = scenes.instanced_field(args.instances, args.width, args.height, args.max_depth, seed=2,
+                                       spheres_per_blas=args.spheres)
+    else:
+        scene = scenes.sphere_field(args.spheres, args.width, args.height, args.max_depth, seed=1)
     desc = scene.desc()
-    tris = sum(desc.shapes[i].num_faces for i in range(desc.num_shapes) if desc.shapes[i].kind == 0)
-    n_prims = 0
+    n_prims = tris = 0
     for i in range(desc.num_instances):
         s = desc.shapes[desc.instances[i].shape]
         n_prims += 1 if s.kind == 1 else s.num_faces
+        tris += 0 if s.kind == 1 else s.num_faces
 
     pt = PTPass(device=local_rank)
     pt.set_scene(desc)
@@ -170,9 +188,11 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (procedural sphere field, PCG64 seed 1)",
-            "config": {"workload": f"config4: {n_prims:,}-primitive sphere field ({tris:,} tris), "
-                                   f"{args.width}x{args.height}, {args.spp} spp, max_depth {args.max_depth}",
+            "data": ("synthetic (40 instances of a procedural 250k-tri sphere-field BLAS, PCG64 seed 2)"
+                     if args.config == 5 else "synthetic (procedural sphere field, PCG64 seed 1)"),
+            "config": {"workload": (f"config{args.config}: {n_prims:,}-primitive "
+                                    f"{'instanced field' if args.config == 5 else 'sphere field'} ({tris:,} tris), "
+                                    f"{args.width}x{args.height}, {args.spp} spp, max_depth {args.max_depth}"),
                        "frame": f"{args.spp} x PTPass::OnRun", "parallelism": f"tiles{args.tile}x{world}",
                        "rays_per_frame": rays_total / args.steps,
                        "path_samples_per_s": round(args.width * args.height * args.spp / (ms_per_step * 1e-3), 1),
@@ -209,7 +229,8 @@ def pmc_traffic(args):
     --json), committed as profiles/pmc_extend.json; null when absent or taken
     on another configuration."""
     path = os.path.join(HERE, "profiles", "pmc_extend.json")
-    default_cfg = (args.spheres, args.width, args.height, args.spp, args.max_depth) == (500, 1920, 1080, 8, 4)
+    default_cfg = args.config == 4 and \
+        (args.spheres, args.width, args.height, args.spp, args.max_depth) == (500, 1920, 1080, 8, 4)
     if not default_cfg or not os.path.exists(path):
         return None
     try:

@@ -204,8 +204,13 @@ def sphere_field(num_spheres=500, width=1920, height=1080, max_depth=4, seed=1, 
         for c, r, a in zip(centers, radii, albedo):
             m = wd.add_material(W.diffuse(tuple(a)))
             wd.add_instance(s, m, W.transform(scale=(r, r, r), translate=tuple(c)))
-    # closed room around the field (floor, ceiling, four walls: 12 triangles)
-    # so every camera and bounce ray hits geometry, like an interior scene
+    _room_and_light(wd)
+    return wd
+
+
+def _room_and_light(wd: W.World):
+    """Closed room (floor, ceiling, four walls: 12 triangles) so every camera and
+    bounce ray hits geometry, a 3x3 area light under the ceiling, the camera."""
     rect = wd.add_builtin("rectangle")
     wall_m = wd.add_material(W.twosided(W.diffuse((0.6, 0.6, 0.6))))
     room = [((8, 12, 1), ((1, 0, 0), -90), (0, 0, 2)),     # floor      y = 0
@@ -221,6 +226,42 @@ def sphere_field(num_spheres=500, width=1920, height=1080, max_depth=4, seed=1, 
                     emitter_radiance=(40.0, 38.0, 34.0))
     cam = W.look_at_mitsuba((0.0, 6.0, 13.0), (0.0, 4.6, 0.0), (0, 1, 0))
     wd.set_sensor(50.0, cam, fov_axis="y")
+
+
+def blas_mesh(num_spheres=125, seed=2, box=4.0, slices=40, stacks=26):
+    """One object-space mesh of ``num_spheres`` 2,000-triangle spheres (config 3
+    generator, centred at the origin): the 250k-triangle BLAS of config 5."""
+    centers, radii, _ = _field_geometry(num_spheres, seed, box)
+    centers = centers - np.array([0.0, box / 2, 0.0])
+    v, nrm, uv, idx = uv_sphere(slices, stacks)
+    P = np.concatenate([v * r + c for c, r in zip(centers, radii)])
+    N = np.concatenate([nrm for _ in radii])
+    T = np.concatenate([uv for _ in radii])
+    I = np.concatenate([idx + k * len(v) for k in range(len(radii))])
+    return P.astype(np.float32), I.astype(np.uint32), N.astype(np.float32), T.astype(np.float32)
+
+
+def instanced_field(num_instances=40, width=3840, height=2160, max_depth=6, seed=2, spheres_per_blas=125,
+                    slices=40, stacks=26) -> W.World:
+    """Config 5: ``num_instances`` instances of one 250k-triangle BLAS under random
+    rigid transforms (seed 2), alternating rough dielectric (alpha 0.35) and rough
+    plastic (alpha 0.35), material_test.xml parameters, inside the config-4 room."""
+    wd = W.World()
+    wd.set_film(width, height, max_depth)
+    pos, idx, nrm, uv = blas_mesh(spheres_per_blas, seed, 4.0, slices, stacks)
+    blas = wd.add_mesh(pos, idx, nrm, uv)
+    m_diel = wd.add_material(W.rough_dielectric(alpha=0.35, int_ior=1.5, ext_ior=1.0))
+    m_plas = wd.add_material(W.rough_plastic(alpha=0.35, diffuse_reflectance=(0.647814, 0.647814, 0.647814),
+                                             int_ior=1.5, ext_ior=1.0))
+    rng = np.random.Generator(np.random.PCG64(seed))
+    for k in range(num_instances):
+        axis = rng.normal(size=3)
+        axis /= np.linalg.norm(axis)
+        angle = float(rng.uniform(0.0, 360.0))
+        t = (float(rng.uniform(-5.0, 5.0)), float(rng.uniform(2.5, 11.5)), float(rng.uniform(-7.0, 8.0)))
+        wd.add_instance(blas, m_diel if k % 2 == 0 else m_plas,
+                        W.transform(rotate=(tuple(axis), angle), translate=t))
+    _room_and_light(wd)
     return wd
 
 

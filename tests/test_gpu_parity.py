@@ -286,3 +286,17 @@ def test_non_accumulating_frame_overwrites():
     a = render_gpu(desc, 1, seed=5, accumulate=False)
     b = render_gpu(desc, 1, seed=5, accumulate=False, prev=np.full((32 * 32, 4), 7.0, np.float32))
     assert np.array_equal(a["pt accum buffer"], b["pt accum buffer"])
+
+
+def test_instanced_rough_materials_parity():
+    """Config 5 in miniature: instances of one BLAS under rigid transforms, rough dielectric +
+    rough plastic, depth 6 (scenes.instanced_field)."""
+    w = scenes.instanced_field(num_instances=6, width=160, height=90, max_depth=6, seed=2, spheres_per_blas=12)
+    desc = w.desc()
+    gpu = render_gpu(desc, 4)
+    ref = oracle.OracleScene(desc).render(spp=4)
+    exact = compare(gpu, ref, "instanced6x12")
+    s, rs = gpu["stats"], ref["stats"]
+    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
+        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
+    assert exact == 160 * 90
