@@ -9,8 +9,10 @@
  *                              (example/path_tracer/pt_pass.cpp:29-37,107-209;
  *                               framework/world/gas_manager.cpp:61-185, ias_manager.cpp:29-114)
  *   pupil_pt_set_camera      — CameraHelper::GetCudaMemory upload (framework/world/camera.cpp:72-91)
- *   pupil_pt_update_instance — IASManager::UpdateInstance + IAS::Update refit
- *                              (framework/world/ias_manager.cpp:116-151,187-211)
+ *   pupil_pt_update_instance — IASManager::UpdateInstance + IAS::Update
+ *                              (framework/world/ias_manager.cpp:116-151,187-211); the engine
+ *                              rebuilds its (flattened) BVH over the moved primitives
+ *   pupil_pt_update_emitters — EmitterHelper reset on RenderInstanceUpdate (world/world.cpp:45-54)
  *   pupil_pt_render          — PTPass::OnRun: optixLaunch(w,h,1) + sync, repeated spp times
  *                              with random_seed++ / sample_cnt += accumulate
  *                              (example/path_tracer/pt_pass.cpp:39-57, main.cu:36-194)
@@ -230,7 +232,11 @@ int pupil_abi_version(void);
 
 int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out);
 int pupil_pt_set_camera(pupil_pt *pt, const float sample_to_camera[16], const float camera_to_world[16]);
+/* instance = index into pupil_scene_desc.instances; to_world / to_object row-major 3x4.
+ * Must not overlap a render in flight (the reference serialises both under its render mutex). */
 int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_world[12], const float to_object[12]);
+/* replaces the area-emitter table, selection CDF and env emitter (after an emissive instance moved) */
+int pupil_pt_update_emitters(pupil_pt *pt, const pupil_scene_desc *scene);
 int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_launch *launch, void *hip_stream);
 int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out);
 int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank,
@@ -266,6 +272,10 @@ int pupil_world_add_instance(pupil_world *w, uint32_t shape, uint32_t material, 
                              uint32_t flip_normals, uint32_t flip_tex_coords, uint32_t is_emitter,
                              const pupil_texture *radiance, uint32_t *out_instance);
 int pupil_world_add_const_env(pupil_world *w, const float radiance[3]);
+/* RenderInstanceUpdate on the host side: new to_world (row-major 4x4) of instance `instance`
+ * (index into pupil_scene_desc.instances); the next pupil_world_get_desc has the new
+ * instance matrices and area emitters (world/world.cpp:45-54) */
+int pupil_world_set_instance_transform(pupil_world *w, uint32_t instance, const float to_world[16]);
 /* resolves emitters (EmitterHelper), camera matrices (CameraHelper) and fills desc;
  * pointers stay valid until the world is modified or destroyed */
 int pupil_world_get_desc(pupil_world *w, pupil_scene_desc *desc);

@@ -96,6 +96,7 @@ SIGNATURES = {
     "pupil_pt_create": (C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "pupil_pt_set_camera": (C.c_int, [C.c_void_p, f32p, f32p]),
     "pupil_pt_update_instance": (C.c_int, [C.c_void_p, C.c_uint32, f32p, f32p]),
+    "pupil_pt_update_emitters": (C.c_int, [C.c_void_p, C.POINTER(SceneDesc)]),
     "pupil_pt_render": (C.c_int, [C.c_void_p, C.POINTER(Frame), C.POINTER(Launch), C.c_void_p]),
     "pupil_pt_stats": (C.c_int, [C.c_void_p, C.POINTER(Counters)]),
     "pupil_pt_local_pixels": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
@@ -113,6 +114,7 @@ SIGNATURES = {
     "pupil_world_add_instance": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, f32p, C.c_uint32,
                                            C.c_uint32, C.c_uint32, C.POINTER(Texture), u32p]),
     "pupil_world_add_const_env": (C.c_int, [C.c_void_p, f32p]),
+    "pupil_world_set_instance_transform": (C.c_int, [C.c_void_p, C.c_uint32, f32p]),
     "pupil_world_get_desc": (C.c_int, [C.c_void_p, C.POINTER(SceneDesc)]),
     "pupil_world_destroy": (None, [C.c_void_p]),
 }

@@ -1030,6 +1030,20 @@ int pupil_world_add_instance(pupil_world *w, uint32_t shape, uint32_t material, 
     return PUPIL_OK;
 }
 
+int pupil_world_set_instance_transform(pupil_world *w, uint32_t instance, const float to_world[16]) {
+    if (!w || !to_world) return Pupil::werr(PUPIL_ERR_INVALID, "null argument");
+    // desc instance k = k-th scene instance with a shape (World::Build skips the others)
+    uint32_t k = 0;
+    for (auto &ins : w->w.scene.instances) {
+        if (ins.shape < 0) continue;
+        if (k++ == instance) {
+            std::memcpy(ins.transform.matrix.e, to_world, sizeof(ins.transform.matrix.e));
+            return PUPIL_OK;
+        }
+    }
+    return Pupil::werr(PUPIL_ERR_INVALID, "instance out of range");
+}
+
 int pupil_world_add_const_env(pupil_world *w, const float radiance[3]) {
     if (!w || !radiance) return Pupil::werr(PUPIL_ERR_INVALID, "null argument");
     Pupil::resource::SceneEmitter e;

@@ -37,6 +37,13 @@ private:
     float m_c2w[16] = {};
 };
 
+class World;
+// payload of EWorldEvent::RenderInstanceUpdate
+struct InstanceUpdate {
+    World *world;
+    uint32_t instance;  // index into Desc().instances
+};
+
 class World {
 public:
     std::unique_ptr<SceneInfo> scene;
@@ -50,6 +57,9 @@ public:
     bool LoadScene(const std::filesystem::path &xml) noexcept;
     // Programmatic scenes: the caller filled `handle()` through pupil_world_*.
     bool Finalize() noexcept;
+    // Moves instance `instance` (row-major 4x4), refreshes Desc() (instance
+    // matrices, area emitters) and fires EWorldEvent::RenderInstanceUpdate.
+    bool SetInstanceTransform(uint32_t instance, const float to_world[16]) noexcept;
 
     pupil_world *handle() noexcept { return m_world; }
     // Flattened scene for pupil_pt_create (valid until the world changes).

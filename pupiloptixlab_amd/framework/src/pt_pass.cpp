@@ -106,7 +106,18 @@ bool PTPass::Stats(pupil_pt_counters &out) noexcept { return m_engine && pupil_p
 
 void PTPass::BindingEventCallback() noexcept {
     EventBinder<EWorldEvent::CameraChange>([this](void *) { m_dirty = true; });
-    EventBinder<EWorldEvent::RenderInstanceUpdate>([this](void *) { m_dirty = true; });
+    EventBinder<EWorldEvent::RenderInstanceUpdate>([this](void *p) {
+        // IAS update + emitter reset (ias_manager.cpp:116-151, world.cpp:45-54), then restart accumulation
+        const auto *u = static_cast<const world::InstanceUpdate *>(p);
+        if (u && u->world == m_world && m_engine) {
+            const pupil_instance &ins = m_world->Desc().instances[u->instance];
+            if (pupil_pt_update_instance(m_engine, u->instance, ins.to_world, ins.to_object) != PUPIL_OK)
+                Log("%s: instance update failed: %s", name.c_str(), pupil_last_error());
+            else if (ins.emitter_offset >= 0 && pupil_pt_update_emitters(m_engine, &m_world->Desc()) != PUPIL_OK)
+                Log("%s: emitter update failed: %s", name.c_str(), pupil_last_error());
+        }
+        m_dirty = true;
+    });
     EventBinder<ESystemEvent::SceneLoad>([this](void *p) { SetScene(static_cast<world::World *>(p)); });
 }
 

@@ -49,4 +49,15 @@ bool World::Finalize() noexcept {
     return true;
 }
 
+bool World::SetInstanceTransform(uint32_t instance, const float to_world[16]) noexcept {
+    if (!m_world || pupil_world_set_instance_transform(m_world, instance, to_world) != PUPIL_OK) {
+        Log("instance update failed: %s", pupil_last_error());
+        return false;
+    }
+    if (!Finalize()) return false;
+    InstanceUpdate u{this, instance};
+    EventDispatcher<EWorldEvent::RenderInstanceUpdate>(&u);
+    return true;
+}
+
 }  // namespace Pupil::world

@@ -103,8 +103,25 @@ class PTPass(Pass):
         self.tile = (32, 0, 1)  # tile_size, rank, world
         self.events = events or Events()
         self.events.bind(Events.CAMERA_CHANGE, lambda _: self.mark_dirty())
-        self.events.bind(Events.RENDER_INSTANCE_UPDATE, lambda _: self.mark_dirty())
+        self.events.bind(Events.RENDER_INSTANCE_UPDATE, self._on_instance_update)
         self.events.bind(Events.SCENE_LOAD, lambda w: self.set_scene(w))
+
+    def _on_instance_update(self, arg):
+        if arg is not None:
+            self.update_instance(*arg)
+        else:
+            self.mark_dirty()
+
+    def update_instance(self, world, instance: int):
+        """RenderInstanceUpdate: push instance `instance`'s new transform from `world`
+        (already moved with World.set_instance_transform) into the engine, and the
+        emitter table when the instance is emissive; restarts accumulation."""
+        desc = world.desc()
+        ins = desc.instances[instance]
+        check(self._lib.pupil_pt_update_instance(self._pt, int(instance), ins.to_world, ins.to_object))
+        if ins.emitter_offset >= 0:
+            check(self._lib.pupil_pt_update_emitters(self._pt, C.byref(desc)))
+        self.dirty = True
 
     # ---- inspector knobs (pt_pass.cpp:225-237)
     @property
@@ -253,7 +270,7 @@ class System:
         if isinstance(p, PTPass):
             p.events = self.events
             self.events.bind(Events.CAMERA_CHANGE, lambda _: p.mark_dirty())
-            self.events.bind(Events.RENDER_INSTANCE_UPDATE, lambda _: p.mark_dirty())
+            self.events.bind(Events.RENDER_INSTANCE_UPDATE, p._on_instance_update)
             self.events.bind(Events.SCENE_LOAD, lambda w: p.set_scene(w))
 
     def set_scene(self, world):

@@ -191,6 +191,13 @@ class World:
         self._desc = None
         return out.value
 
+    def set_instance_transform(self, instance: int, to_world):
+        """Move instance `instance` (index into desc().instances); the next desc()
+        carries the new matrices and area emitters (world/world.cpp:45-54)."""
+        m = _f32(to_world, 16)
+        check(self._lib.pupil_world_set_instance_transform(self._h, int(instance), _ptr(m)))
+        self._desc = None
+
     def add_const_env(self, radiance):
         r = _f32(radiance, 3)
         check(self._lib.pupil_world_add_const_env(self._h, _ptr(r)))
