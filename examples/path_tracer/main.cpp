@@ -1,10 +1,10 @@
 // examples/path_tracer/main.cpp — headless counterpart of the reference's
 // example/path_tracer/main.cpp: System + PTPass + an XML scene, rendered for
 // a fixed number of frames (the reference loops until the window closes),
-// then "final result" is written as a PFM (rows bottom-up, which is the
-// reference's pixel order: row 0 is the image bottom).
+// then "final result" is written with pupil_image_save (.exr / .hdr like
+// util::BitmapTexture::Save, or .pfm).
 //
-// usage: pupil_path_tracer <scene.xml> [frames=16] [out.pfm] [device=0]
+// usage: pupil_path_tracer <scene.xml> [frames=16] [out.exr|.hdr|.pfm] [device=0]
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -13,22 +13,9 @@
 #include "pupil/framework.h"
 #include "pupil/pt_pass.h"
 
-static bool write_pfm(const char *path, const float *rgba, int w, int h) {
-    FILE *f = std::fopen(path, "wb");
-    if (!f) return false;
-    std::fprintf(f, "PF\n%d %d\n-1.0\n", w, h);
-    std::vector<float> row(3 * (size_t)w);
-    for (int y = 0; y < h; y++) {
-        for (int x = 0; x < w; x++)
-            for (int c = 0; c < 3; c++) row[3 * x + c] = rgba[4 * ((size_t)y * w + x) + c];
-        std::fwrite(row.data(), sizeof(float), row.size(), f);
-    }
-    return std::fclose(f) == 0;
-}
-
 int main(int argc, char **argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s <scene.xml> [frames=16] [out.pfm] [device=0]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s <scene.xml> [frames=16] [out.exr|.hdr|.pfm] [device=0]\n", argv[0]);
         return 2;
     }
     const int frames = argc > 2 ? std::atoi(argv[2]) : 16;
@@ -51,7 +38,8 @@ int main(int argc, char **argv) {
             if (!buf || hipMemcpy(host.data(), buf->cuda_ptr, host.size() * sizeof(float), hipMemcpyDeviceToHost) !=
                             hipSuccess) {
                 rc = 1;
-            } else if (out[0] && !write_pfm(out, host.data(), w, h)) {
+            } else if (out[0] && pupil_image_save(out, (uint32_t)w, (uint32_t)h, host.data(), PUPIL_IMAGE_AUTO) != PUPIL_OK) {
+                Pupil::Log("%s", pupil_last_error());
                 rc = 1;
             }
             if (rc == 0) {

@@ -252,6 +252,13 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
  * out[6*i + k] for k in that order (bit-exactness probe for the CPU oracle) */
 int pupil_debug_math(int device, uint32_t n, const float *x, const float *y2, float *out);
 
+/* ---- image output (util::BitmapTexture::Save, framework/util/texture.cpp:12-85,152-160) ----
+ * rgba: width*height float4, row 0 = image bottom (the "final result" order).
+ * EXR: uncompressed FLOAT B,G,R, top row first; HDR: Radiance RGBE, top row first;
+ * PFM: float RGB, bottom row first.  format PUPIL_IMAGE_AUTO picks by extension. */
+enum { PUPIL_IMAGE_AUTO = 0, PUPIL_IMAGE_EXR = 1, PUPIL_IMAGE_HDR = 2, PUPIL_IMAGE_PFM = 3 };
+int pupil_image_save(const char *path, uint32_t width, uint32_t height, const float *rgba, uint32_t format);
+
 /* ---- host world (the reference's resource::Scene + world::World, C++ inside) ---- */
 typedef struct pupil_world pupil_world;
 

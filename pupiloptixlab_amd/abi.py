@@ -15,7 +15,9 @@ MAT_CONDUCTOR, MAT_ROUGH_CONDUCTOR, MAT_PLASTIC, MAT_ROUGH_PLASTIC = 4, 5, 6, 7
 EMITTER_NONE, EMITTER_TRI_AREA, EMITTER_SPHERE, EMITTER_CONST_ENV, EMITTER_ENV_MAP = 0, 1, 2, 3, 4
 SHAPE_MESH, SHAPE_SPHERE = 0, 1
 
-PUPIL_OK = 0
+PUPIL_OK = OK = 0
+ERR_INVALID, ERR_HIP, ERR_OOM, ERR_IO, ERR_UNSUPPORTED = -1, -2, -3, -4, -5
+IMAGE_AUTO, IMAGE_EXR, IMAGE_HDR, IMAGE_PFM = 0, 1, 2, 3
 ERR_NAMES = {-1: "PUPIL_ERR_INVALID", -2: "PUPIL_ERR_HIP", -3: "PUPIL_ERR_OOM", -4: "PUPIL_ERR_IO",
              -5: "PUPIL_ERR_UNSUPPORTED"}
 
@@ -104,6 +106,7 @@ SIGNATURES = {
     "pupil_pt_destroy": (None, [C.c_void_p]),
     "pupil_pt_trace_rays": (C.c_int, [C.c_void_p, C.c_uint32, f32p, f32p, C.c_int]),
     "pupil_debug_math": (C.c_int, [C.c_int, C.c_uint32, f32p, f32p, f32p]),
+    "pupil_image_save": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, f32p, C.c_uint32]),
     "pupil_world_create": (C.c_int, [C.POINTER(C.c_void_p)]),
     "pupil_world_load_xml": (C.c_int, [C.c_void_p, C.c_char_p]),
     "pupil_world_set_film": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]),

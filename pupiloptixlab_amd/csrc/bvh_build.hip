@@ -13,6 +13,7 @@
 //   7. k_emit          64 B BVH2 nodes; subtrees of <= leaf_size primitives
 //                      collapse into one leaf (their primitives are contiguous)
 //   8. k_reorder       primitive records in Morton order (leaf ranges index them)
+//   9. k_attrs         per-primitive shading records in the same order
 #include <hip/hip_runtime.h>
 
 #include <vector>
@@ -435,6 +436,51 @@ __global__ void k_emit4(int n, const uint32_t *sorted_vals, const Aabb *prim_box
     nodes4[idx4[i]] = o;
 }
 
+// Shading record of each primitive in traversal (Morton) order, kAttrStride
+// float4 per primitive: everything the hit reconstruction of
+// Geometry::GetHitLocalGeometry (render/geometry.h:48-96) gathers from the
+// object-space mesh, in one 128-B line instead of index + 3 x position / normal /
+// uv gathers:  [0] p0 | global id (+ sphere bit)  [1] p1 | instance  [2] p2 | n0.x
+// [3] n0.yz n1.xy  [4] n1.z n2.xyz  [5] t0 t1  [6] t2 | 0 0  [7] unused
+__global__ void k_attrs(int n, const uint32_t *sorted_vals, BvhBuildInput in, float4 *attrs) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t prim = sorted_vals[i];
+    const uint32_t inst_id = in.prim_inst[prim];
+    const DevInstance &inst = in.instances[inst_id];
+    float4 *r = attrs + (size_t)kAttrStride * i;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (inst.kind == PUPIL_SHAPE_SPHERE) {
+        r[0] = make_float4(0.f, 0.f, 0.f, __uint_as_float(prim | kPrimSphereBit));
+        r[1] = make_float4(0.f, 0.f, 0.f, __uint_as_float(inst_id));
+        r[2] = r[3] = r[4] = r[5] = r[6] = r[7] = z;
+        return;
+    }
+    const uint32_t local = prim - inst.prim_offset;
+    const uint32_t i0 = inst.indices[3 * local], i1 = inst.indices[3 * local + 1], i2 = inst.indices[3 * local + 2];
+    const float *P = inst.positions;
+    r[0] = make_float4(P[3 * i0], P[3 * i0 + 1], P[3 * i0 + 2], __uint_as_float(prim));
+    r[1] = make_float4(P[3 * i1], P[3 * i1 + 1], P[3 * i1 + 2], __uint_as_float(inst_id));
+    float nn[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (inst.normals) {
+        const float *N = inst.normals;
+        const uint32_t id[3] = {i0, i1, i2};
+        for (int v = 0; v < 3; v++)
+            for (int c = 0; c < 3; c++) nn[3 * v + c] = N[3 * id[v] + c];
+    }
+    r[2] = make_float4(P[3 * i2], P[3 * i2 + 1], P[3 * i2 + 2], nn[0]);
+    r[3] = make_float4(nn[1], nn[2], nn[3], nn[4]);
+    r[4] = make_float4(nn[5], nn[6], nn[7], nn[8]);
+    if (inst.texcoords) {
+        const float *T = inst.texcoords;
+        r[5] = make_float4(T[2 * i0], T[2 * i0 + 1], T[2 * i1], T[2 * i1 + 1]);
+        r[6] = make_float4(T[2 * i2], T[2 * i2 + 1], 0.f, 0.f);
+    } else {
+        r[5] = r[6] = z;
+    }
+    r[7] = z;
+}
+
 __global__ void k_reorder(int n, const uint32_t *sorted_vals, const float4 *recs_in, float4 *recs_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -455,9 +501,11 @@ void free_lbvh(BvhBuildOutput &out) {
     if (out.nodes) (void)hipFree(out.nodes);
     if (out.nodes4) (void)hipFree(out.nodes4);
     if (out.prims) (void)hipFree(out.prims);
+    if (out.attrs) (void)hipFree(out.attrs);
     out.nodes = nullptr;
     out.nodes4 = nullptr;
     out.prims = nullptr;
+    out.attrs = nullptr;
 }
 
 int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms) {
@@ -499,6 +547,7 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     if (!err) err = dmalloc(&parent_leaf, n);
     if (!err) err = dmalloc(&out.nodes, n > 1 ? (size_t)(n - 1) : 1);
     if (!err) err = dmalloc(&out.prims, 3 * (size_t)n);
+    if (!err) err = dmalloc(&out.attrs, (size_t)kAttrStride * n);
     if (err) {
         free_lbvh(out);
     } else {
@@ -553,6 +602,7 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
             out.num_nodes4 = 0;
         }
         hipLaunchKernelGGL(k_reorder, dim3(g), dim3(kBlock), 0, s, n, vi, recs, out.prims);
+        hipLaunchKernelGGL(k_attrs, dim3(g), dim3(kBlock), 0, s, n, vi, in, out.attrs);
         out.num_nodes = n > 1 ? (uint32_t)(n - 1) : 0u;
         out.root_link = ((uint32_t)n <= leaf_size) ? (uint32_t)make_leaf(0u, (uint32_t)n) : 0u;
         out.root_link4 = out.root_link;

@@ -471,6 +471,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     DeviceScene &sc = pt->sc;
     sc.nodes = pt->bvh.nodes;
     sc.prims = pt->bvh.prims;
+    sc.attrs = pt->bvh.attrs;
     sc.num_prims = pt->num_prims;
     sc.root_link = pt->bvh.root_link;
     sc.nodes4 = pt->bvh.nodes4;
@@ -535,6 +536,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     pt->bvh = nb;
     pt->sc.nodes = nb.nodes;
     pt->sc.prims = nb.prims;
+    pt->sc.attrs = nb.attrs;
     pt->sc.root_link = nb.root_link;
     pt->sc.nodes4 = nb.nodes4;
     pt->sc.root_link4 = nb.root_link4;

@@ -110,6 +110,7 @@ struct BvhBuildOutput {
     BvhNode *nodes;     // device, max(1, n-1)
     Bvh4Node *nodes4;   // device, collapsed 4-wide quantized tree
     float4 *prims;      // device, 3 * n
+    float4 *attrs;      // device, kAttrStride * n shading records (same order)
     uint32_t root_link;
     uint32_t root_link4;
     uint32_t num_nodes;

@@ -726,12 +726,14 @@ struct HitGeo {
 };
 
 // __closesthit__default (main.cu:216-230) + Geometry::GetHitLocalGeometry
-// (render/geometry.h:272-320), from the compact hit record.
+// (render/geometry.h:272-320), from the compact hit record and the primitive's
+// shading record (bvh_build.hip k_attrs: object-space vertices, normals, uvs).
 __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, vec3 ro, vec3 rd, vec2 stale_uv) {
     HitGeo out;
     const uint32_t idx = __float_as_uint(h.w);
-    const float4 a = sc.prims[3 * idx + 0];
-    const float4 b = sc.prims[3 * idx + 1];
+    const float4 *rec = sc.attrs + (size_t)kAttrStride * idx;
+    const float4 a = rec[0];
+    const float4 b = rec[1];
     const uint32_t ref = __float_as_uint(a.w);
     const uint32_t gprim = ref & ~kPrimSphereBit;
     const uint32_t inst_id = __float_as_uint(b.w);
@@ -748,21 +750,20 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, v
         if (in.flip_normals) g.normal = g.normal * -1.f;
     } else {
         local = gprim - in.prim_offset;
-        const uint32_t i0 = in.indices[3 * local + 0], i1 = in.indices[3 * local + 1], i2 = in.indices[3 * local + 2];
-        const float *P = in.positions;
-        const vec3 p0 = v3(P[3 * i0], P[3 * i0 + 1], P[3 * i0 + 2]);
-        const vec3 p1 = v3(P[3 * i1], P[3 * i1 + 1], P[3 * i1 + 2]);
-        const vec3 p2 = v3(P[3 * i2], P[3 * i2 + 1], P[3 * i2 + 2]);
+        const float4 c = rec[2];
+        const vec3 p0 = v3(a.x, a.y, a.z);
+        const vec3 p1 = v3(b.x, b.y, b.z);
+        const vec3 p2 = v3(c.x, c.y, c.z);
         const float u = h.y, v = h.z;
         const float w = 1.f - u - v;
         g.position = w * p0 + u * p1 + v * p2;
         g.position = xform_point(in.to_world, g.position);
         vec3 n;
         if (in.normals) {
-            const float *N = in.normals;
-            const vec3 n0 = v3(N[3 * i0], N[3 * i0 + 1], N[3 * i0 + 2]);
-            const vec3 n1 = v3(N[3 * i1], N[3 * i1 + 1], N[3 * i1 + 2]);
-            const vec3 n2 = v3(N[3 * i2], N[3 * i2 + 1], N[3 * i2 + 2]);
+            const float4 d = rec[3], e = rec[4];
+            const vec3 n0 = v3(c.w, d.x, d.y);
+            const vec3 n1 = v3(d.z, d.w, e.x);
+            const vec3 n2 = v3(e.y, e.z, e.w);
             n = w * n0 + u * n1 + v * n2;
         } else {
             n = cross(p1 - p0, p2 - p0);
@@ -770,11 +771,11 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, v
         g.normal = normalize(xform_normal(in.to_object, n));
         if (in.flip_normals) g.normal = g.normal * -1.f;
         if (in.texcoords) {
-            const float *T = in.texcoords;
-            const vec2 t0 = v2(T[2 * i0], T[2 * i0 + 1]);
-            const vec2 t1 = v2(T[2 * i1], T[2 * i1 + 1]);
-            const vec2 t2 = v2(T[2 * i2], T[2 * i2 + 1]);
-            g.texcoord = w * t0 + u * t1 + v * t2;
+            const float4 t01 = rec[5], t2 = rec[6];
+            const vec2 t0 = v2(t01.x, t01.y);
+            const vec2 t1 = v2(t01.z, t01.w);
+            const vec2 tt2 = v2(t2.x, t2.y);
+            g.texcoord = w * t0 + u * t1 + v * tt2;
             if (in.flip_tex_coords) g.texcoord.y = 1.f - g.texcoord.y;
         }
     }

@@ -112,6 +112,7 @@ PT_HD uint32_t leaf_first(int link) { return ((uint32_t)~link) >> 3; }
 PT_HD uint32_t leaf_count(int link) { return (((uint32_t)~link) & 7u) + 1u; }
 
 constexpr uint32_t kPrimSphereBit = 0x80000000u;
+constexpr uint32_t kAttrStride = 8;  // float4 per shading record (one 128-B line)
 
 struct Camera {
     float s2c[16];  // sample_to_camera, row-major (mat4x4 r0..r3)
@@ -122,6 +123,7 @@ struct DeviceScene {
     const BvhNode *nodes;
     const Bvh4Node *nodes4;
     const float4 *prims;  // 3 float4 per primitive, Morton order
+    const float4 *attrs;  // kAttrStride float4 per primitive, same order (hit reconstruction)
     uint32_t num_prims;
     uint32_t root_link;   // link of the root (internal 0 or a leaf), BVH2
     uint32_t root_link4;  // same for the BVH4
