@@ -16,6 +16,9 @@
 //   9. k_attrs         per-primitive shading records in the same order
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+#include <utility>
 #include <vector>
 
 #include "pt_kernels.h"
@@ -323,6 +326,208 @@ __global__ void k_emit(int n, const uint32_t *sorted_vals, const Aabb *prim_boxe
     nodes[i] = nd;
 }
 
+// ---------------------------------------------------------------- PLOC
+// Parallel locally-ordered clustering (Meister & Bittner 2018) over the
+// Morton-ordered primitives: each cluster finds its nearest neighbour (smallest
+// union surface area, ties to the smaller index) within +-kPlocRadius
+// positions, mutual pairs merge, the cluster list is compacted in order, and
+// this repeats until one cluster is left.  It yields a tree of markedly lower
+// SAH cost than the Karras hierarchy over the same order.  The result is
+// converted to the LBVH arrays (children / ranges / parents / node boxes, root
+// 0, subtrees contiguous in a new primitive order) so emit and the BVH4
+// collapse are shared.  Refs: >= 0 internal node (creation id), < 0 leaf ~pos.
+constexpr int kPlocRadius = 16;
+constexpr int kScanBlock = 1024;
+constexpr int kScanItems = 4;
+
+__device__ __forceinline__ float half_area(const Aabb &b) {
+    const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+__global__ void k_ploc_init(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, int *ref, Aabb *box) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    ref[i] = ~i;
+    box[i] = prim_boxes[sorted_vals[i]];
+}
+
+__global__ __launch_bounds__(kBlock) void k_ploc_nn(int m, const Aabb *box, int *nn) {
+    __shared__ Aabb tile[kBlock + 2 * kPlocRadius];
+    const int base = blockIdx.x * kBlock - kPlocRadius;
+    for (int t = threadIdx.x; t < kBlock + 2 * kPlocRadius; t += kBlock) {
+        const int j = base + t;
+        if (j >= 0 && j < m) tile[t] = box[j];
+    }
+    __syncthreads();
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= m) return;
+    const Aabb bi = tile[threadIdx.x + kPlocRadius];
+    float best = __builtin_huge_valf();
+    int bj = -1;
+    const int j0 = max(0, i - kPlocRadius), j1 = min(m - 1, i + kPlocRadius);
+    for (int j = j0; j <= j1; j++) {
+        if (j == i) continue;
+        const float a = half_area(merge(bi, tile[j - base]));
+        if (a < best) {  // ascending j: ties keep the smaller index
+            best = a;
+            bj = j;
+        }
+    }
+    nn[i] = bj;
+}
+
+// per cluster: low word = survives (1), high word = creates a node (1)
+__global__ void k_ploc_flags(int m, const int *nn, unsigned long long *flags) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int j = nn[i];
+    const bool mutual = nn[j] == i;
+    const unsigned long long keep = (mutual && i > j) ? 0ull : 1ull;
+    const unsigned long long make = (mutual && i < j) ? 1ull : 0ull;
+    flags[i] = keep | (make << 32);
+}
+
+// exclusive scan of 64-bit counts: block pass, block-sum pass, add pass
+__global__ __launch_bounds__(kScanBlock) void k_scan64_blocks(unsigned long long *data, int n,
+                                                            unsigned long long *sums) {
+    __shared__ unsigned long long wsum[kScanBlock / 64];
+    const int base = blockIdx.x * kScanBlock * kScanItems + threadIdx.x * kScanItems;
+    unsigned long long v[kScanItems], tsum = 0;
+    for (int k = 0; k < kScanItems; k++) {
+        v[k] = base + k < n ? data[base + k] : 0ull;
+        tsum += v[k];
+    }
+    unsigned long long inc = tsum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long u = __shfl_up(inc, o);
+        if ((int)__lane_id() >= o) inc += u;
+    }
+    if (__lane_id() == 63) wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const unsigned long long w = threadIdx.x < kScanBlock / 64 ? wsum[threadIdx.x] : 0ull;
+        unsigned long long winc = w;
+        for (int o = 1; o < kScanBlock / 64; o <<= 1) {
+            const unsigned long long u = __shfl_up(winc, o);
+            if ((int)threadIdx.x >= o) winc += u;
+        }
+        if (threadIdx.x < kScanBlock / 64) wsum[threadIdx.x] = winc - w;
+        if (threadIdx.x == kScanBlock / 64 - 1) sums[blockIdx.x] = winc;
+    }
+    __syncthreads();
+    unsigned long long run = wsum[threadIdx.x >> 6] + inc - tsum;
+    for (int k = 0; k < kScanItems; k++) {
+        if (base + k < n) data[base + k] = run;
+        run += v[k];
+    }
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_scan64_sums(unsigned long long *sums, int nb,
+                                                          unsigned long long *total) {
+    // nb <= kScanBlock * kScanItems: reuse the block pass on a single block
+    __shared__ unsigned long long wsum[kScanBlock / 64];
+    const int base = threadIdx.x * kScanItems;
+    unsigned long long v[kScanItems], tsum = 0;
+    for (int k = 0; k < kScanItems; k++) {
+        v[k] = base + k < nb ? sums[base + k] : 0ull;
+        tsum += v[k];
+    }
+    unsigned long long inc = tsum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long u = __shfl_up(inc, o);
+        if ((int)__lane_id() >= o) inc += u;
+    }
+    if (__lane_id() == 63) wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const unsigned long long w = threadIdx.x < kScanBlock / 64 ? wsum[threadIdx.x] : 0ull;
+        unsigned long long winc = w;
+        for (int o = 1; o < kScanBlock / 64; o <<= 1) {
+            const unsigned long long u = __shfl_up(winc, o);
+            if ((int)threadIdx.x >= o) winc += u;
+        }
+        if (threadIdx.x < kScanBlock / 64) wsum[threadIdx.x] = winc - w;
+        if (threadIdx.x == kScanBlock / 64 - 1) *total = winc;
+    }
+    __syncthreads();
+    unsigned long long run = wsum[threadIdx.x >> 6] + inc - tsum;
+    for (int k = 0; k < kScanItems; k++) {
+        if (base + k < nb) sums[base + k] = run;
+        run += v[k];
+    }
+}
+
+__global__ void k_scan64_add(unsigned long long *data, int n, const unsigned long long *sums) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    data[i] += sums[i / (kScanBlock * kScanItems)];
+}
+
+__global__ void k_ploc_compact(int m, const int *ref, const Aabb *box, const int *nn,
+                               const unsigned long long *flags, const unsigned long long *pos, int base_id,
+                               int *ref_out, Aabb *box_out, int2 *node_child, Aabb *node_box, int *node_count) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const unsigned long long f = flags[i];
+    if (!(f & 1ull)) return;
+    const unsigned long long p = pos[i];
+    const int out = (int)(p & 0xFFFFFFFFull);
+    if (f >> 32) {
+        const int j = nn[i];
+        const int id = base_id + (int)(p >> 32);
+        const Aabb b = merge(box[i], box[j]);
+        const int a = ref[i], c = ref[j];
+        node_child[id] = make_int2(a, c);
+        node_box[id] = b;
+        node_count[id] = (a >= 0 ? node_count[a] : 1) + (c >= 0 ? node_count[c] : 1);
+        ref_out[out] = id;
+        box_out[out] = b;
+    } else {
+        ref_out[out] = ref[i];
+        box_out[out] = box[i];
+    }
+}
+
+// top-down: subtree [first, first + count) of the new primitive order
+__global__ void k_ploc_place(int lo, int hi, const int2 *node_child, const int *node_count, int *first,
+                             int *newpos) {
+    const int id = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= hi) return;
+    const int f = first[id];
+    const int2 c = node_child[id];
+    const int cl = c.x >= 0 ? node_count[c.x] : 1;
+    if (c.x >= 0) first[c.x] = f;
+    else newpos[~c.x] = f;
+    if (c.y >= 0) first[c.y] = f + cl;
+    else newpos[~c.y] = f + cl;
+}
+
+// creation id -> LBVH arrays (root 0), new primitive order
+__global__ void k_ploc_export(int n, const int2 *node_child, const Aabb *node_box, const int *node_count,
+                              const int *first, const int *newpos, int2 *children, int2 *ranges, Aabb *node_boxes,
+                              int *parent_internal, int *parent_leaf) {
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n - 1) return;
+    const int fid = (n - 2) - id;
+    const int2 c = node_child[id];
+    const int a = c.x >= 0 ? (n - 2) - c.x : ~newpos[~c.x];
+    const int b = c.y >= 0 ? (n - 2) - c.y : ~newpos[~c.y];
+    children[fid] = make_int2(a, b);
+    ranges[fid] = make_int2(first[id], first[id] + node_count[id] - 1);
+    node_boxes[fid] = node_box[id];
+    if (a >= 0) parent_internal[a] = fid;
+    else parent_leaf[~a] = fid;
+    if (b >= 0) parent_internal[b] = fid;
+    else parent_leaf[~b] = fid;
+}
+
+__global__ void k_ploc_permute(int n, const int *newpos, const uint32_t *vals_in, uint32_t *vals_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    vals_out[newpos[i]] = vals_in[i];
+}
+
 // ---------------------------------------------------------------- BVH4 collapse
 // Binary nodes at even depth become 4-wide nodes whose children are their
 // grandchildren (or the child itself where the child is a leaf).
@@ -495,6 +700,77 @@ hipError_t dmalloc(T **p, size_t count) {
     return hipMalloc((void **)p, sizeof(T) * (count > 0 ? count : 1));
 }
 
+// PLOC topology (see the PLOC section) -> LBVH arrays and the new primitive order
+hipError_t build_ploc(int n, const uint32_t *vals_in, uint32_t *vals_out, const Aabb *prim_boxes, int2 *children,
+                      int2 *ranges, Aabb *node_boxes, int *parent_internal, int *parent_leaf, hipStream_t s) {
+    int *ref_a = nullptr, *ref_b = nullptr, *nn = nullptr, *node_count = nullptr, *first = nullptr, *newpos = nullptr;
+    Aabb *box_a = nullptr, *box_b = nullptr, *node_box = nullptr;
+    int2 *node_child = nullptr;
+    unsigned long long *flg = nullptr, *pos = nullptr, *sums = nullptr, *total = nullptr;
+    const int per = kScanBlock * kScanItems;
+    const int nsum = (n + per - 1) / per;
+    hipError_t err = dmalloc(&ref_a, n);
+    if (!err) err = dmalloc(&ref_b, n);
+    if (!err) err = dmalloc(&nn, n);
+    if (!err) err = dmalloc(&node_count, n);
+    if (!err) err = dmalloc(&first, n);
+    if (!err) err = dmalloc(&newpos, n);
+    if (!err) err = dmalloc(&box_a, n);
+    if (!err) err = dmalloc(&box_b, n);
+    if (!err) err = dmalloc(&node_box, n);
+    if (!err) err = dmalloc(&node_child, n);
+    if (!err) err = dmalloc(&flg, n);
+    if (!err) err = dmalloc(&pos, n);
+    if (!err) err = dmalloc(&sums, nsum);
+    if (!err) err = dmalloc(&total, 1);
+    if (!err && nsum > per) err = hipErrorInvalidValue;  // > 16.7 G primitives
+    std::vector<int2> iters;
+    if (!err) {
+        const auto grid = [](int m) { return dim3((unsigned)((m + kBlock - 1) / kBlock)); };
+        hipLaunchKernelGGL(k_ploc_init, grid(n), dim3(kBlock), 0, s, n, vals_in, prim_boxes, ref_a, box_a);
+        int m = n, base = 0;
+        while (m > 1 && !err) {
+            hipLaunchKernelGGL(k_ploc_nn, grid(m), dim3(kBlock), 0, s, m, box_a, nn);
+            hipLaunchKernelGGL(k_ploc_flags, grid(m), dim3(kBlock), 0, s, m, nn, flg);
+            (void)hipMemcpyAsync(pos, flg, sizeof(unsigned long long) * m, hipMemcpyDeviceToDevice, s);
+            const int nb = (m + per - 1) / per;
+            hipLaunchKernelGGL(k_scan64_blocks, dim3(nb), dim3(kScanBlock), 0, s, pos, m, sums);
+            hipLaunchKernelGGL(k_scan64_sums, dim3(1), dim3(kScanBlock), 0, s, sums, nb, total);
+            hipLaunchKernelGGL(k_scan64_add, grid(m), dim3(kBlock), 0, s, pos, m, sums);
+            unsigned long long tot = 0;
+            (void)hipMemcpyAsync(&tot, total, sizeof(tot), hipMemcpyDeviceToHost, s);
+            err = hipStreamSynchronize(s);
+            const int m_new = (int)(tot & 0xFFFFFFFFull), merges = (int)(tot >> 32);
+            if (!err && (merges <= 0 || m_new != m - merges)) err = hipErrorUnknown;  // cannot happen
+            if (err) break;
+            hipLaunchKernelGGL(k_ploc_compact, grid(m), dim3(kBlock), 0, s, m, ref_a, box_a, nn, flg, pos, base,
+                               ref_b, box_b, node_child, node_box, node_count);
+            iters.push_back(make_int2(base, merges));
+            base += merges;
+            std::swap(ref_a, ref_b);
+            std::swap(box_a, box_b);
+            m = m_new;
+        }
+        if (!err) {
+            (void)hipMemsetAsync(first + (n - 2), 0, sizeof(int), s);  // root = last node created
+            for (size_t k = iters.size(); k-- > 0;) {
+                const int lo = iters[k].x, hi = iters[k].x + iters[k].y;
+                hipLaunchKernelGGL(k_ploc_place, grid(hi - lo), dim3(kBlock), 0, s, lo, hi, node_child, node_count,
+                                   first, newpos);
+            }
+            hipLaunchKernelGGL(k_ploc_export, grid(n - 1), dim3(kBlock), 0, s, n, node_child, node_box, node_count,
+                               first, newpos, children, ranges, node_boxes, parent_internal, parent_leaf);
+            hipLaunchKernelGGL(k_ploc_permute, grid(n), dim3(kBlock), 0, s, n, newpos, vals_in, vals_out);
+            err = hipStreamSynchronize(s);
+        }
+    }
+    void *bufs[] = {ref_a, ref_b, nn, node_count, first, newpos, box_a, box_b, node_box, node_child, flg, pos,
+                    sums, total};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    return err;
+}
+
 }  // namespace
 
 void free_lbvh(BvhBuildOutput &out) {
@@ -571,10 +847,19 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
             (void)hipMemsetAsync(parent_internal, 0xFF, sizeof(int) * n, s);
             (void)hipMemsetAsync(flags, 0, sizeof(uint32_t) * n, s);
             const uint32_t gi = (uint32_t)((n - 1 + kBlock - 1) / kBlock);
-            hipLaunchKernelGGL(k_karras, dim3(gi), dim3(kBlock), 0, s, ki, n, children, ranges, parent_internal,
-                               parent_leaf);
-            hipLaunchKernelGGL(k_refit, dim3(g), dim3(kBlock), 0, s, n, vi, boxes, children, parent_internal,
-                               parent_leaf, node_boxes, flags);
+            const char *builder = std::getenv("PUPIL_BVH_BUILDER");
+            const bool ploc = !(builder && std::strcmp(builder, "lbvh") == 0);
+            if (ploc) {
+                err = build_ploc(n, vi, vo, boxes, children, ranges, node_boxes, parent_internal, parent_leaf, s);
+                uint32_t *t = vi;  // vo holds the PLOC primitive order
+                vi = vo;
+                vo = t;
+            } else {
+                hipLaunchKernelGGL(k_karras, dim3(gi), dim3(kBlock), 0, s, ki, n, children, ranges, parent_internal,
+                                   parent_leaf);
+                hipLaunchKernelGGL(k_refit, dim3(g), dim3(kBlock), 0, s, n, vi, boxes, children, parent_internal,
+                                   parent_leaf, node_boxes, flags);
+            }
             hipLaunchKernelGGL(k_emit, dim3(gi), dim3(kBlock), 0, s, n, vi, boxes, children, ranges, node_boxes,
                                leaf_size, out.nodes);
             // 4-wide quantized tree: depth parity -> flags -> compact indices -> nodes
