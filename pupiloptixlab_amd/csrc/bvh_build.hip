@@ -641,6 +641,102 @@ __global__ void k_emit4(int n, const uint32_t *sorted_vals, const Aabb *prim_box
     nodes4[idx4[i]] = o;
 }
 
+// ---------------------------------------------------------------- greedy BVH4 collapse
+// Top-down, one level of 4-wide nodes per pass: a 4-wide node starts from its
+// binary node's two children and repeatedly opens the child with the largest
+// surface area (an internal binary node that is not a leaf-sized subtree) until
+// it has four children (the wide-BVH collapse of Wald et al. 2008 / Ylitie et
+// al. 2017).  Children that remain internal become the next level's 4-wide
+// nodes, numbered breadth-first after a scan of their counts.
+__device__ __forceinline__ bool opens(int c, const int2 *ranges, uint32_t leaf_size) {
+    if (c < 0) return false;
+    const int2 r = ranges[c];
+    return (uint32_t)(r.y - r.x + 1) > leaf_size;
+}
+
+__global__ void k_collapse_pick(int items, const int *item_node, const int2 *children, const int2 *ranges,
+                                const Aabb *node_boxes, uint32_t leaf_size, int4 *clist,
+                                unsigned long long *inner_count) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= items) return;
+    const int b = item_node[t];
+    int c[4];
+    const int2 ch = children[b];
+    c[0] = ch.x;
+    c[1] = ch.y;
+    int nk = 2;
+    while (nk < 4) {
+        int best = -1;
+        float best_a = -1.f;
+        for (int k = 0; k < nk; k++)
+            if (opens(c[k], ranges, leaf_size)) {
+                const float a = half_area(node_boxes[c[k]]);
+                if (a > best_a) {
+                    best_a = a;
+                    best = k;
+                }
+            }
+        if (best < 0) break;
+        const int2 g = children[c[best]];
+        c[best] = g.x;
+        c[nk++] = g.y;
+    }
+    unsigned long long inner = 0;
+    for (int k = 0; k < nk; k++) inner += opens(c[k], ranges, leaf_size) ? 1ull : 0ull;
+    for (int k = nk; k < 4; k++) c[k] = kEmptyLink;
+    clist[t] = make_int4(c[0], c[1], c[2], c[3]);
+    inner_count[t] = inner;
+}
+
+__global__ void k_collapse_emit(int items, int base, int next_base, const int *item_node, const int4 *clist,
+                                const unsigned long long *inner_pos, const uint32_t *sorted_vals,
+                                const Aabb *prim_boxes, const int2 *ranges, const Aabb *node_boxes,
+                                uint32_t leaf_size, int *next_items, Bvh4Node *nodes4) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= items) return;
+    const int4 cl = clist[t];
+    const int cc[4] = {cl.x, cl.y, cl.z, cl.w};
+    int link[4];
+    float clo[3][4], chi[3][4];
+    int nk = 0;
+    int pos = (int)inner_pos[t];
+    for (int k = 0; k < 4; k++) {
+        const int c = cc[k];
+        if (c == kEmptyLink) break;
+        Aabb b;
+        if (c < 0) {
+            link[nk] = make_leaf((uint32_t)~c, 1u);
+            b = prim_boxes[sorted_vals[~c]];
+        } else if (!opens(c, ranges, leaf_size)) {
+            const int2 r = ranges[c];
+            link[nk] = make_leaf((uint32_t)r.x, (uint32_t)(r.y - r.x + 1));
+            b = node_boxes[c];
+        } else {
+            next_items[pos] = c;
+            link[nk] = next_base + pos;
+            pos++;
+            b = node_boxes[c];
+        }
+        for (int a = 0; a < 3; a++) {
+            clo[a][nk] = b.lo[a];
+            chi[a][nk] = b.hi[a];
+        }
+        nk++;
+    }
+    for (int k = nk; k < 4; k++)
+        for (int a = 0; a < 3; a++) clo[a][k] = chi[a][k] = 0.f;
+    const Aabb nb = node_boxes[item_node[t]];
+    Bvh4Node o;
+    uint32_t ex, ey, ez;
+    quantize_axis(nb.lo[0], nb.hi[0], clo[0], chi[0], nk, o.ox, ex, o.qlo_x, o.qhi_x);
+    quantize_axis(nb.lo[1], nb.hi[1], clo[1], chi[1], nk, o.oy, ey, o.qlo_y, o.qhi_y);
+    quantize_axis(nb.lo[2], nb.hi[2], clo[2], chi[2], nk, o.oz, ez, o.qlo_z, o.qhi_z);
+    o.exps = ex | (ey << 8) | (ez << 16);
+    for (int k = 0; k < 4; k++) o.child[k] = k < nk ? link[k] : kEmptyLink;
+    o.pad[0] = o.pad[1] = 0u;
+    nodes4[base + t] = o;
+}
+
 // Shading record of each primitive in traversal (Morton) order, kAttrStride
 // float4 per primitive: everything the hit reconstruction of
 // Geometry::GetHitLocalGeometry (render/geometry.h:48-96) gathers from the
@@ -698,6 +794,49 @@ __global__ void k_reorder(int n, const uint32_t *sorted_vals, const float4 *recs
 template <typename T>
 hipError_t dmalloc(T **p, size_t count) {
     return hipMalloc((void **)p, sizeof(T) * (count > 0 ? count : 1));
+}
+
+// Greedy breadth-first BVH4 collapse (k_collapse_pick / k_collapse_emit);
+// nodes4 must hold n - 1 entries; returns the number of 4-wide nodes.
+hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
+                         const int2 *ranges, const Aabb *node_boxes, uint32_t leaf_size, Bvh4Node *nodes4,
+                         uint32_t *num_nodes4, hipStream_t s) {
+    int *items_a = nullptr, *items_b = nullptr;
+    int4 *clist = nullptr;
+    unsigned long long *cnt = nullptr, *sums = nullptr, *total = nullptr;
+    const int per = kScanBlock * kScanItems;
+    const int cap = n;  // a level never has more 4-wide nodes than binary internal nodes
+    hipError_t err = dmalloc(&items_a, cap);
+    if (!err) err = dmalloc(&items_b, cap);
+    if (!err) err = dmalloc(&clist, cap);
+    if (!err) err = dmalloc(&cnt, cap);
+    if (!err) err = dmalloc(&sums, (cap + per - 1) / per);
+    if (!err) err = dmalloc(&total, 1);
+    int base = 0, items = 1;
+    if (!err) err = hipMemsetAsync(items_a, 0, sizeof(int), s);  // binary root 0
+    const auto grid = [](int m) { return dim3((unsigned)((m + kBlock - 1) / kBlock)); };
+    while (!err && items > 0) {
+        hipLaunchKernelGGL(k_collapse_pick, grid(items), dim3(kBlock), 0, s, items, items_a, children, ranges,
+                           node_boxes, leaf_size, clist, cnt);
+        const int nb = (items + per - 1) / per;
+        hipLaunchKernelGGL(k_scan64_blocks, dim3(nb), dim3(kScanBlock), 0, s, cnt, items, sums);
+        hipLaunchKernelGGL(k_scan64_sums, dim3(1), dim3(kScanBlock), 0, s, sums, nb, total);
+        hipLaunchKernelGGL(k_scan64_add, grid(items), dim3(kBlock), 0, s, cnt, items, sums);
+        hipLaunchKernelGGL(k_collapse_emit, grid(items), dim3(kBlock), 0, s, items, base, base + items, items_a, clist,
+                           cnt, sorted_vals, prim_boxes, ranges, node_boxes, leaf_size, items_b, nodes4);
+        unsigned long long tot = 0;
+        (void)hipMemcpyAsync(&tot, total, sizeof(tot), hipMemcpyDeviceToHost, s);
+        err = hipStreamSynchronize(s);
+        base += items;
+        items = (int)tot;
+        if (base + items > n - 1) err = hipErrorUnknown;  // cannot happen
+        std::swap(items_a, items_b);
+    }
+    *num_nodes4 = (uint32_t)base;
+    void *bufs[] = {items_a, items_b, clist, cnt, sums, total};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    return err;
 }
 
 // PLOC topology (see the PLOC section) -> LBVH arrays and the new primitive order
@@ -862,6 +1001,14 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
             }
             hipLaunchKernelGGL(k_emit, dim3(gi), dim3(kBlock), 0, s, n, vi, boxes, children, ranges, node_boxes,
                                leaf_size, out.nodes);
+            const char *collapse = std::getenv("PUPIL_BVH4_COLLAPSE");
+            if (!err && !(collapse && std::strcmp(collapse, "parity") == 0)) {
+                // 4-wide quantized tree, greedy surface-area collapse
+                err = dmalloc(&out.nodes4, (size_t)(n - 1));
+                if (!err)
+                    err = collapse_bvh4(n, vi, boxes, children, ranges, node_boxes, leaf_size, out.nodes4,
+                                        &out.num_nodes4, s);
+            } else if (!err) {
             // 4-wide quantized tree: depth parity -> flags -> compact indices -> nodes
             uint32_t *depth = ko, *flags4 = vo, *idx4 = nullptr;  // the sort's free ping-pong buffers
             err = dmalloc(&idx4, n);
@@ -882,6 +1029,7 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
                                    flags4, idx4, leaf_size, out.nodes4);
             (void)hipStreamSynchronize(s);
             if (idx4) (void)hipFree(idx4);
+            }
         } else {
             err = dmalloc(&out.nodes4, 1);
             out.num_nodes4 = 0;

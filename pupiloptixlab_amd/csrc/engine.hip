@@ -89,6 +89,7 @@ struct pupil_pt {
     BvhBuildOutput bvh{};
     uint32_t width = 0, height = 0, max_depth = 1;
     uint32_t num_prims = 0;
+    uint32_t leaf_size = 3;  // primitives per BVH leaf (PUPIL_LEAF_SIZE)
     double build_ms = 0.0;
     // path state / queues (grown on demand)
     size_t cap = 0;
@@ -466,7 +467,9 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     pt->d_prim_inst = d_prim_inst;
     // LBVH (replaces GAS + IAS builds)
     BvhBuildInput bin{pt->num_prims, d_prim_inst, d_insts, d_mats};
-    if (build_lbvh(bin, pt->bvh, 4u, pt->own_stream, &pt->build_ms) != 0)
+    pt->leaf_size = 3u;
+    if (const char *ls = std::getenv("PUPIL_LEAF_SIZE")) pt->leaf_size = (uint32_t)std::min(8, std::max(1, std::atoi(ls)));
+    if (build_lbvh(bin, pt->bvh, pt->leaf_size, pt->own_stream, &pt->build_ms) != 0)
         return cleanup(fail(PUPIL_ERR_HIP, "LBVH build failed"));
     DeviceScene &sc = pt->sc;
     sc.nodes = pt->bvh.nodes;
@@ -528,7 +531,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     BvhBuildInput bin{pt->num_prims, pt->d_prim_inst, pt->d_insts, pt->d_mats};
     BvhBuildOutput nb{};
     double ms = 0.0;
-    if (build_lbvh(bin, nb, 4u, pt->own_stream, &ms) != 0) {
+    if (build_lbvh(bin, nb, pt->leaf_size, pt->own_stream, &ms) != 0) {
         free_lbvh(nb);
         return fail(PUPIL_ERR_HIP, "LBVH rebuild failed");
     }
