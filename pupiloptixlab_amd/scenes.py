@@ -267,3 +267,60 @@ def instanced_field(num_instances=40, width=3840, height=2160, max_depth=6, seed
 
 def triangle_count(num_spheres, slices=40, stacks=26):
     return num_spheres * 2 * slices * (stacks - 1) + 14
+
+
+def _write_pfm(path: str, rgb: np.ndarray):
+    """rgb: (h, w, 3) float32, row 0 = top (written bottom-up as PFM requires)."""
+    h, w, _ = rgb.shape
+    with open(path, "wb") as f:
+        f.write(f"PF\n{w} {h}\n-1.0\n".encode())
+        f.write(np.ascontiguousarray(rgb[::-1], dtype="<f4").tobytes())
+
+
+def textured_env_xml(path: str, width=320, height=240, max_depth=5, seed=4) -> str:
+    """Scene-input fidelity scene: an env-map emitter
+    (PFM, rotated, scaled; world/emitter.cpp:107-149 CDF), bitmap textures with
+    point and bilinear filtering and a to_uv scale (cuda/texture.cpp:60-102),
+    a checkerboard, a small area light, open sky so the env map is seen and
+    sampled.  The PFM files are written next to the XML."""
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    eh, ew = 32, 64
+    yy, xx = np.mgrid[0:eh, 0:ew].astype(np.float32)
+    env = np.stack([0.3 + 0.7 * (1 - yy / eh), 0.4 + 0.3 * np.sin(xx / ew * 6.283), 0.5 + 0.5 * yy / eh], -1)
+    env[4:7, 40:44] = (30.0, 25.0, 18.0)  # a sun
+    _write_pfm(os.path.join(d, "env.pfm"), env.astype(np.float32))
+    _write_pfm(os.path.join(d, "tex.pfm"), rng.uniform(0.1, 0.9, (16, 16, 3)).astype(np.float32))
+    lines = [
+        '<scene version="3.0.0">',
+        f'  <integrator type="path"><integer name="max_depth" value="{max_depth}"/></integrator>',
+        '  <sensor type="perspective"><float name="fov" value="45"/><string name="fov_axis" value="y"/>',
+        '    <transform name="to_world"><lookat origin="0, 2.2, 6" target="0, 0.8, 0" up="0, 1, 0"/></transform>',
+        f'    <film type="hdrfilm"><integer name="width" value="{width}"/><integer name="height" value="{height}"/>'
+        '</film>',
+        '  </sensor>',
+        '  <emitter type="envmap"><string name="filename" value="env.pfm"/><float name="scale" value="1.5"/>',
+        '    <transform name="to_world"><rotate y="1" angle="30"/></transform></emitter>',
+        '  <shape type="rectangle"><transform name="to_world"><scale x="6" y="6" z="1"/>'
+        '<rotate x="1" angle="-90"/></transform>',
+        '    <bsdf type="diffuse"><texture type="bitmap" name="reflectance"><string name="filename" value="tex.pfm"/>'
+        '<string name="filter_type" value="nearest"/><transform name="to_uv"><scale x="3" y="3"/></transform>'
+        '</texture></bsdf></shape>',
+        '  <shape type="sphere"><point name="center" x="-1.2" y="1" z="0"/><float name="radius" value="1"/>',
+        '    <bsdf type="diffuse"><texture type="bitmap" name="reflectance"><string name="filename" value="tex.pfm"/>'
+        '<string name="filter_type" value="bilinear"/></texture></bsdf></shape>',
+        '  <shape type="sphere"><point name="center" x="1.2" y="0.8" z="0.3"/><float name="radius" value="0.8"/>',
+        '    <bsdf type="roughplastic"><float name="alpha" value="0.2"/><float name="int_ior" value="1.5"/>'
+        '<float name="ext_ior" value="1"/><texture type="checkerboard" name="diffuse_reflectance">'
+        '<rgb name="color0" value="0.8, 0.2, 0.1"/><rgb name="color1" value="0.1, 0.2, 0.7"/>'
+        '<transform name="to_uv"><scale x="4" y="4"/></transform></texture></bsdf></shape>',
+        '  <shape type="rectangle"><transform name="to_world"><scale x="0.4" y="0.4" z="1"/>'
+        '<rotate x="1" angle="90"/><translate x="0" y="3.5" z="1"/></transform>',
+        '    <bsdf type="diffuse"><rgb name="reflectance" value="0, 0, 0"/></bsdf>',
+        '    <emitter type="area"><rgb name="radiance" value="12, 11, 9"/></emitter></shape>',
+        '</scene>',
+    ]
+    with open(path, "w") as f:
+        f.write("\n".join(lines))
+    return path

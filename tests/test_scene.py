@@ -160,3 +160,16 @@ def test_sphere_field_generator_counts():
         faces = sum(d.shapes[d.instances[i].shape].num_faces if d.shapes[d.instances[i].shape].kind == 0 else 1
                     for i in range(d.num_instances))
         assert faces == scenes.triangle_count(n)
+
+
+def test_env_map_and_bitmap_textures_load(tmp_path):
+    from pupiloptixlab_amd import abi, scenes
+
+    p = scenes.textured_env_xml(str(tmp_path / "texenv.xml"), 64, 48, 5)
+    d = World().load_scene(p).desc()
+    assert d.env and d.env.contents.type == abi.EMITTER_ENV_MAP
+    assert d.env.contents.radiance.width == 64 and d.env.contents.radiance.height == 32
+    assert abs(d.env.contents.scale - 1.5) < 1e-7
+    kinds = [(d.materials[i].tex[0].type, d.materials[i].tex[0].filter) for i in range(d.num_materials)]
+    assert (abi.TEX_BITMAP, 0) in kinds and (abi.TEX_BITMAP, 1) in kinds
+    assert any(d.materials[i].tex[1].type == abi.TEX_CHECKERBOARD for i in range(d.num_materials))
