@@ -127,7 +127,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ext_ms = trace_ms = shade_ms = 0.0
-    ext_launches = 0
+    ext_launches = trace_launches = 0
     rays_local = 0
     for _ in range(args.steps):
         frame()
@@ -135,6 +135,7 @@ def main():
         ext_ms += st["extend_ms"]
         ext_launches += st["extend_launches"]
         trace_ms += st["trace_ms"]
+        trace_launches += st["trace_launches"]
         shade_ms += st["shade_ms"]
         rays_local += st["primary_rays"] + st["extension_rays"] + st["shadow_rays"]
     torch.cuda.synchronize(dev)
@@ -156,13 +157,15 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     mrays = rays_total / elapsed / 1e6
     rays_frame_local = st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"]
-    # roofline of the dominant kernel, the closest-hit traversal (extend):
-    # algorithmic bytes per SURVEY.md §8(d) = 32 B ray + 16 B hit + 64 B per
-    # node visit + 48 B per primitive test, counted in the instrumented frame,
-    # per launch; divided by the average extend launch time measured with HIP
-    # events on the render stream over the timed frames
-    per_launch_bytes = st_bytes["extend_bytes"] / max(1, st_bytes["extend_launches"])
-    per_launch_ms = ext_ms / max(1, ext_launches)
+    # roofline of the dominant kernel, the persistent BVH4 traversal k_trace4
+    # (per frame: the primary extend launch, then one launch per bounce over
+    # the concatenated extension + shadow lists): algorithmic bytes per SURVEY.md
+    # §8(d) = 32 B ray + 16 B hit + 64 B per node visit + 48 B per primitive
+    # test, counted in the instrumented frame, per launch; divided by the
+    # average traversal launch time measured with HIP events on the render
+    # stream over the timed frames
+    per_launch_bytes = st_bytes["trace_bytes"] / max(1, st_bytes["trace_launches"])
+    per_launch_ms = trace_ms / max(1, trace_launches)
     achieved_gbs = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
     traffic = pmc_traffic(args)
 
@@ -208,12 +211,13 @@ def main():
                            int(st_bytes["shadow_rays"]),
                            round((st_bytes["node_visits"] - st_bytes["extend_node_visits"]) / max(1, st_bytes["shadow_rays"]), 2),
                            round((st_bytes["prim_tests"] - st_bytes["extend_prim_tests"]) / max(1, st_bytes["shadow_rays"]), 2)],
-                       "stage_ms_per_frame": {"extend": round(ext_ms / args.steps, 3),
-                                              "shadow": round((trace_ms - ext_ms) / args.steps, 3),
+                       "stage_ms_per_frame": {"primary_extend": round(ext_ms / args.steps, 3),
+                                              "bounce_trace": round((trace_ms - ext_ms) / args.steps, 3),
                                               "shade": round(shade_ms / args.steps, 3)}},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_trace4<extend> (closest-hit BVH4 traversal)",
+                         "kernel": "k_trace4 (persistent BVH4 traversal, all launches: primary extend + "
+                                   "per-bounce extension+shadow)",
                          "bytes_per_launch": round(per_launch_bytes, 1),
                          "ms_per_launch": round(per_launch_ms, 4)},
             "cpu_baseline": cpu,

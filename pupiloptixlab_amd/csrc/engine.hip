@@ -90,6 +90,7 @@ struct pupil_pt {
     uint32_t width = 0, height = 0, max_depth = 1;
     uint32_t num_prims = 0;
     uint32_t leaf_size = 3;  // primitives per BVH leaf (PUPIL_LEAF_SIZE)
+    bool mixed_trace = true;  // one persistent launch per bounce for shadow + extension rays (PUPIL_MIXED)
     double build_ms = 0.0;
     // path state / queues (grown on demand)
     size_t cap = 0;
@@ -487,6 +488,8 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     sc.num_cus = (uint32_t)std::max(1, cus);
     sc.trace_refill = 40;  // persistent BVH4 kernels; 0 selects the one-ray-per-lane kernels (A/B)
     if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
+    pt->mixed_trace = true;
+    if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
     sc.trace_node_min = 4;
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     sc.prim_inst = d_prim_inst;
@@ -663,13 +666,20 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
             if (b < 128)
                 HIP_TRY(hipMemcpyAsync(pt->ray_log + 2 * b, q.counts + kCntNext, 2 * sizeof(uint32_t),
                                        hipMemcpyDeviceToDevice, s));
-            ev0(1);
-            launch_shadow(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);
-            ev1();
-            HIP_TRY(hipMemsetAsync(pt->ps.mbin, 0xFF, np, s));
-            ev0(0);
-            launch_extend(pt->sc, pt->ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, tsp, s);
-            ev1();
+            if (pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill) {
+                HIP_TRY(hipMemsetAsync(pt->ps.mbin, 0xFF, np, s));
+                ev0(1);
+                launch_trace_mixed(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);
+                ev1();
+            } else {
+                ev0(1);
+                launch_shadow(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);
+                ev1();
+                HIP_TRY(hipMemsetAsync(pt->ps.mbin, 0xFF, np, s));
+                ev0(0);
+                launch_extend(pt->sc, pt->ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, tsp, s);
+                ev1();
+            }
             bin_paths();
         }
     }

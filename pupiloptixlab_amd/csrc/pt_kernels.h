@@ -88,6 +88,9 @@ void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState 
                   uint32_t bounce, hipStream_t s);
 void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                    const TraceStats *stats, hipStream_t s);
+// one persistent launch over the next + shadow lists of a bounce (BVH4 persistent path only)
+void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
+                        const TraceStats *stats, hipStream_t s);
 void launch_accumulate(const FrameParams &fp, const PathState &ps, hipStream_t s);
 uint32_t trace_grid_blocks();
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,

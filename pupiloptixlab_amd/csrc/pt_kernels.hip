@@ -147,11 +147,12 @@ __device__ __forceinline__ bool traverse(const DeviceScene &sc, const RayPre &r,
     return found;
 }
 
-// Leaf intersection shared by both node formats.
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool intersect_leaf(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
-                                               float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
-                                               float &bb2, uint32_t &prims_tested, bool &found) {
+// Leaf intersection shared by both node formats.  any = terminate on the first
+// hit (shadow ray); a compile-time constant except in the mixed persistent kernel.
+template <bool STATS>
+__device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
+                                                   float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
+                                                   float &bb2, uint32_t &prims_tested, bool &found, bool any) {
     const uint32_t first = leaf_first(leaf);
     const uint32_t count = leaf_count(leaf);
     for (uint32_t i = first; i < first + count; i++) {
@@ -171,7 +172,7 @@ __device__ __forceinline__ bool intersect_leaf(const DeviceScene &sc, const RayP
                                      b2);
         }
         if (hit) {
-            if (ANY) {
+            if (any) {
                 found = true;
                 return true;
             }
@@ -186,6 +187,13 @@ __device__ __forceinline__ bool intersect_leaf(const DeviceScene &sc, const RayP
         }
     }
     return false;
+}
+
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool intersect_leaf(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
+                                               float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
+                                               float &bb2, uint32_t &prims_tested, bool &found) {
+    return intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, bb1, bb2, prims_tested, found, ANY);
 }
 
 __device__ __forceinline__ void cswap(float &ta, int &la, float &tb, int &lb) {
@@ -430,7 +438,10 @@ __device__ __forceinline__ void csel(float &ta, int &la, float &tb, int &lb) {
     lb = l1;
 }
 
-enum TraceMode : int { kModeExtend = 0, kModeShadow = 1, kModeRays = 2 };
+// kModeMixed: one launch over the concatenated next + shadow lists of a bounce
+// (q.nxsh[0, cnt_next) extension rays, then cnt_shadow shadow rays), so each
+// bounce pays one persistent-kernel tail instead of two.
+enum TraceMode : int { kModeExtend = 0, kModeShadow = 1, kModeRays = 2, kModeMixed = 3 };
 
 struct TraceJob {
     const uint32_t *queue;      // extend: path ids (null = identity)
@@ -521,15 +532,18 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                                                         int *ovf, uint32_t ovf_threads, TraceStats stats) {
     constexpr float kInf = __builtin_huge_valf();
     __shared__ int s_ring[kRing * kTraceBlock];
+    const uint32_t n_next = MODE == kModeMixed ? q.counts[kCntNext] : 0u;
     const uint32_t count =
-        MODE == kModeShadow ? q.counts[kCntShadow] : (job.count_ptr ? *job.count_ptr : job.static_count);
+        MODE == kModeShadow ? q.counts[kCntShadow]
+                            : (MODE == kModeMixed ? n_next + q.counts[kCntShadow]
+                                                  : (job.count_ptr ? *job.count_ptr : job.static_count));
     const uint32_t *shadow_q = MODE == kModeShadow ? q.nxsh + q.counts[kStartShadow] : nullptr;
     RingStack st;
     st.lds = s_ring + threadIdx.x;
     st.ovf = ovf + blockIdx.x * blockDim.x + threadIdx.x;
     st.ovf_stride = ovf_threads;
     st.reset();
-    uint32_t nv = 0, npt = 0;
+    uint32_t nv = 0, npt = 0, nv_sh = 0, npt_sh = 0;  // mixed: shadow-ray counts apart
     // STATS-only SIMD-efficiency diagnostics, each event counted by one lane:
     // node-loop wave iterations / active lanes, leaf-loop iterations / active
     // lanes, refills / lanes refilled
@@ -540,6 +554,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     float tmin = 0.f, tmax = 0.f, b1 = 0.f, b2 = 0.f;
     int node = kSentinel, leaf = 0;
     bool found = false;
+    bool any = ANY;  // this lane's ray terminates on its first hit
     for (;;) {
         // ---- refill idle lanes (one atomic per wave)
         const unsigned long long idle = __ballot(!active);
@@ -569,6 +584,13 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                         d = ps.sh_d[p];
                         tmin = 0.001f;
                         tmax = o.w;
+                    } else if (MODE == kModeMixed) {
+                        p = q.nxsh[i];
+                        any = i >= n_next;
+                        o = any ? ps.sh_o[p] : ps.ray_o[p];
+                        d = any ? ps.sh_d[p] : ps.ray_d[p];
+                        tmin = 0.001f;
+                        tmax = any ? o.w : kMaxDistance;
                     } else {
                         p = i;
                         const float *r8 = job.rays + 8 * (size_t)i;
@@ -602,7 +624,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
             while ((uint32_t)node < (uint32_t)kSentinel) {
                 const Bvh4Node n = sc.nodes4[node];
                 if (STATS) {
-                    nv++;
+                    if (MODE == kModeMixed && any) nv_sh++;
+                    else nv++;
                     const unsigned long long m = __ballot(true);
                     if ((int)lane_id() == __ffsll((long long)m) - 1) {
                         dg[0]++;
@@ -636,17 +659,18 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                         dg[3] += (unsigned long long)__popcll(m);
                     }
                 }
-                if (intersect_leaf<ANY, STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, npt, found))
+                if (intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2,
+                                              MODE == kModeMixed && any ? npt_sh : npt, found, any))
                     break;
                 leaf = node;
                 if (node < 0) node = st.pop();
             }
         }
-        const bool done = active && ((node == kSentinel && leaf >= 0) || (ANY && found));
+        const bool done = active && ((node == kSentinel && leaf >= 0) || (any && found));
         // ---- retire
-        if (MODE == kModeExtend) {
+        if (MODE == kModeExtend || MODE == kModeMixed) {
             uint32_t bin = 0;
-            if (done) {
+            if (done && !any) {
                 ps.hit[p] = make_float4(found ? tmax : -1.f, b1, b2, __uint_as_float(found ? best_idx : kMissIndex));
                 if (found) {
                     const uint32_t mt = __float_as_uint(sc.prims[3 * best_idx + 2].w);
@@ -654,8 +678,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                 }
                 ps.mbin[p] = (uint8_t)bin;  // material bin for the partition
             }
-        } else if (MODE == kModeShadow) {
-            if (done && !found) {  // main.cu:124-139
+        }
+        if (MODE == kModeShadow || MODE == kModeMixed) {
+            if (done && any && !found) {  // main.cu:124-139
                 const float4 c = ps.sh_c[p];
                 float4 L = ps.rad[p];
                 L.x = L.x + c.x;
@@ -663,7 +688,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                 L.z = L.z + c.z;
                 ps.rad[p] = L;
             }
-        } else if (done) {
+        } else if (MODE == kModeRays && done) {
             float *o = job.out + 4 * (size_t)p;
             o[0] = found ? (ANY ? 1.f : tmax) : -1.f;
             o[1] = b1;
@@ -673,6 +698,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
         if (done) active = false;
     }
     flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
+    if (MODE == kModeMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
     if (STATS) {
         for (int k = 0; k < 6; k++) {
             unsigned long long v = dg[k];
@@ -1133,6 +1159,19 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
         else SHADOW(false, 2);
     }
 #undef SHADOW
+}
+
+void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
+                        const TraceStats *stats, hipStream_t s) {
+    TraceStats st = stats ? *stats : TraceStats{nullptr};
+    const TraceJob job{nullptr, nullptr, 0u, q.counts + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
+    const uint32_t blocks = trace4_blocks(sc, ovf_threads);
+    if (stats)
+        hipLaunchKernelGGL((k_trace4<kModeMixed, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                           ovf, ovf_threads, st);
+    else
+        hipLaunchKernelGGL((k_trace4<kModeMixed, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                           ovf, ovf_threads, st);
 }
 
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,

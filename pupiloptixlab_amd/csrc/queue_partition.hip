@@ -7,13 +7,18 @@
 // partition lists the ids of every bin in increasing path order, so the next
 // stage reads and writes path state in runs of consecutive records.
 //
-//   k_part_count    per block tile of 16384 paths: count of each bin (wave ballots)
+//   k_part_count    per block tile of 4 waves x rounds x 64 paths: count of each
+//                   bin (wave ballots); rounds is sized so that a launch has
+//                   about kPartTargetBlocks blocks (a 2M-path shard of an 8-GPU
+//                   frame fills the chip as well as a 16M-path 1-GPU frame)
 //   k_part_scan     one block: exclusive scan of the bin-major histogram,
 //                   per-bin start and count
 //   k_part_scatter  per tile: recount per wave, then rank with ballots and write
 //
 // Modes (PartMode, pt_kernels.h): exclusive (bin = key >> shift, 0xFF none),
 // flags (bit shift + b puts the path in bin b; a path can be in several).
+#include <algorithm>
+
 #include "pt_kernels.h"
 
 namespace pupil {
@@ -21,9 +26,17 @@ namespace pupil {
 namespace {
 
 constexpr int kPartBlock = 256;               // 4 waves
-constexpr int kPartRounds = 64;               // rounds of 64 paths per wave
-constexpr uint32_t kPartWaveItems = 64u * kPartRounds;
-constexpr uint32_t kPartTile = 4u * kPartWaveItems;
+constexpr uint32_t kPartMaxRounds = 64;       // rounds of 64 paths per wave
+constexpr uint32_t kPartTargetBlocks = 2048;
+
+uint32_t part_rounds(uint32_t n) {
+    const uint32_t r = (uint32_t)(((uint64_t)n + 256ull * kPartTargetBlocks - 1) / (256ull * kPartTargetBlocks));
+    return std::max(1u, std::min(kPartMaxRounds, r));
+}
+uint32_t part_blocks(uint32_t n) {
+    const uint32_t tile = 256u * part_rounds(n);
+    return (uint32_t)(((uint64_t)n + tile - 1) / tile);
+}
 
 // key value that is in no bin
 template <int MODE>
@@ -41,10 +54,10 @@ __device__ __forceinline__ unsigned long long lanes_below() { return (1ull << __
 
 template <int MODE>
 __device__ __forceinline__ void count_wave(const uint8_t *keys, uint32_t n, uint32_t nbins, uint32_t shift,
-                                           uint32_t base, uint32_t cnt[kPartMaxBins]) {
+                                           uint32_t base, uint32_t rounds, uint32_t cnt[kPartMaxBins]) {
 #pragma unroll
     for (int b = 0; b < kPartMaxBins; b++) cnt[b] = 0;
-    for (int r = 0; r < kPartRounds; r++) {
+    for (uint32_t r = 0; r < rounds; r++) {
         const uint32_t i = base + (uint32_t)r * 64u + __lane_id();
         const uint32_t k = i < n ? keys[i] : no_key<MODE>();
 #pragma unroll
@@ -55,11 +68,12 @@ __device__ __forceinline__ void count_wave(const uint8_t *keys, uint32_t n, uint
 
 template <int MODE>
 __global__ __launch_bounds__(kPartBlock) void k_part_count(const uint8_t *keys, uint32_t n, uint32_t nbins,
-                                                           uint32_t shift, uint32_t *hist, uint32_t nblk) {
+                                                           uint32_t shift, uint32_t *hist, uint32_t nblk,
+                                                           uint32_t rounds) {
     __shared__ uint32_t s[4][kPartMaxBins];
     const uint32_t wave = threadIdx.x >> 6;
     uint32_t cnt[kPartMaxBins];
-    count_wave<MODE>(keys, n, nbins, shift, blockIdx.x * kPartTile + wave * kPartWaveItems, cnt);
+    count_wave<MODE>(keys, n, nbins, shift, (blockIdx.x * 4u + wave) * 64u * rounds, rounds, cnt);
     if (__lane_id() == 0)
         for (int b = 0; b < kPartMaxBins; b++) s[wave][b] = cnt[b];
     __syncthreads();
@@ -117,12 +131,12 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nbl
 template <int MODE>
 __global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys, uint32_t n, uint32_t nbins,
                                                              uint32_t shift, const uint32_t *hist, uint32_t nblk,
-                                                             uint32_t *out) {
+                                                             uint32_t *out, uint32_t rounds) {
     __shared__ uint32_t s[4][kPartMaxBins];
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t base = blockIdx.x * kPartTile + wave * kPartWaveItems;
+    const uint32_t base = (blockIdx.x * 4u + wave) * 64u * rounds;
     uint32_t off[kPartMaxBins];
-    count_wave<MODE>(keys, n, nbins, shift, base, off);
+    count_wave<MODE>(keys, n, nbins, shift, base, rounds, off);
     if (__lane_id() == 0)
         for (int b = 0; b < kPartMaxBins; b++) s[wave][b] = off[b];
     __syncthreads();
@@ -133,8 +147,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys
         for (uint32_t w = 0; w < wave; w++) o += s[w][b];
         off[b] = o;
     }
-    for (int r = 0; r < kPartRounds; r++) {
-        const uint32_t i = base + (uint32_t)r * 64u + __lane_id();
+    for (uint32_t r = 0; r < rounds; r++) {
+        const uint32_t i = base + r * 64u + __lane_id();
         const uint32_t k = i < n ? keys[i] : no_key<MODE>();
 #pragma unroll
         for (int b = 0; b < kPartMaxBins; b++) {
@@ -149,11 +163,16 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys
 
 }  // namespace
 
-uint32_t partition_hist_entries(uint32_t n) { return kPartMaxBins * ((n + kPartTile - 1) / kPartTile); }
+// part_blocks(m) <= max(kPartTargetBlocks, ceil(m / (256 * kPartMaxRounds))) for every m, a bound
+// that grows with n: the scratch sized for the capacity serves every smaller batch
+uint32_t partition_hist_entries(uint32_t n) {
+    return kPartMaxBins * std::max(kPartTargetBlocks, (n + 256u * kPartMaxRounds - 1) / (256u * kPartMaxRounds));
+}
 
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
                       uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, hipStream_t s) {
-    const uint32_t nblk = (n + kPartTile - 1) / kPartTile;
+    const uint32_t nblk = part_blocks(n);
+    const uint32_t rounds = part_rounds(n);
     if (nblk == 0) {
         (void)hipMemsetAsync(counts_out, 0, sizeof(uint32_t) * nbins, s);
         (void)hipMemsetAsync(starts_out, 0, sizeof(uint32_t) * nbins, s);
@@ -161,10 +180,12 @@ void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode 
         return;
     }
 #define PART_RUN(M)                                                                                                \
-    hipLaunchKernelGGL(k_part_count<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk);    \
+    hipLaunchKernelGGL(k_part_count<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk,      \
+                       rounds);                                                                                    \
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, hist, nblk, nbins, counts_out, starts_out,          \
                        total_out);                                                                                 \
-    hipLaunchKernelGGL(k_part_scatter<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk, out)
+    hipLaunchKernelGGL(k_part_scatter<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk, out, \
+                       rounds)
     switch (mode) {
     case kPartExclusive: PART_RUN(kPartExclusive); break;
     case kPartFlags: PART_RUN(kPartFlags); break;

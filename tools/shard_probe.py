@@ -1,0 +1,57 @@
+"""Strong-scaling probe on ONE GPU: render each rank's tile share of the config-4
+frame (tile t -> rank t % N) in turn and report its ms/frame, so the N-GPU
+frame time (max over ranks, gather excluded) can be predicted before the
+driver's 8-GPU run.
+
+usage: python tools/shard_probe.py [--worlds 1 2 4 8] [--frames 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--spheres", type=int, default=500)
+    ap.add_argument("--tile", type=int, default=32)
+    args = ap.parse_args()
+    import torch
+
+    from pupiloptixlab_amd import scenes
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    desc = scenes.sphere_field(args.spheres, 1920, 1080, 4, seed=1).desc()
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    s = torch.cuda.current_stream()
+    base = None
+    for n in args.worlds:
+        per_rank = []
+        for r in range(n):
+            pt.set_tiling(args.tile, r, n)
+            pt.mark_dirty()
+            pt.render(8, stream=s)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.frames):
+                pt.mark_dirty()
+                pt.render(8, stream=s)
+                pt.stats()
+            torch.cuda.synchronize()
+            per_rank.append((time.perf_counter() - t0) / args.frames * 1e3)
+        worst = max(per_rank)
+        base = base or worst * 1.0
+        print(json.dumps({"world": n, "ms_max": round(worst, 3), "ms_min": round(min(per_rank), 3),
+                          "pred_speedup": round(base / worst, 3), "pred_eff": round(base / worst / n, 3),
+                          "ms_per_rank": [round(x, 3) for x in per_rank]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
