@@ -146,6 +146,20 @@ def test_sphere_field_parity(width, monkeypatch):
     compare(gpu, ref, f"field27-bvh{width}")
 
 
+@pytest.mark.parametrize("mixed", ["0", "1"])
+def test_stage_schedules_parity(mixed, monkeypatch):
+    """Separate shadow and extension launches per bounce, or one mixed launch over both lists."""
+    monkeypatch.setenv("PUPIL_MIXED", mixed)
+    desc = scenes.sphere_field(27, 200, 120, 5, seed=4).desc()
+    gpu = render_gpu(desc, 3)
+    ref = oracle.OracleScene(desc).render(spp=3)
+    exact = compare(gpu, ref, f"schedule-mixed{mixed}")
+    assert exact == 200 * 120
+    s, rs = gpu["stats"], ref["stats"]
+    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
+        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
+
+
 # (PUPIL_BVH_WIDTH, PUPIL_REFILL): BVH2, BVH4 one-ray-per-lane, BVH4 persistent with several refill thresholds
 TRAVERSALS = [("2", "16"), ("4", "0"), ("4", "1"), ("4", "16"), ("4", "64")]
 

@@ -34,22 +34,28 @@ def main():
     base = None
     for n in args.worlds:
         per_rank = []
+        host_ms = []
         for r in range(n):
             pt.set_tiling(args.tile, r, n)
             pt.mark_dirty()
             pt.render(8, stream=s)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            host = 0.0
             for _ in range(args.frames):
                 pt.mark_dirty()
+                h0 = time.perf_counter()
                 pt.render(8, stream=s)
+                host += time.perf_counter() - h0
                 pt.stats()
             torch.cuda.synchronize()
             per_rank.append((time.perf_counter() - t0) / args.frames * 1e3)
+            host_ms.append(host / args.frames * 1e3)
         worst = max(per_rank)
         base = base or worst * 1.0
         print(json.dumps({"world": n, "ms_max": round(worst, 3), "ms_min": round(min(per_rank), 3),
                           "pred_speedup": round(base / worst, 3), "pred_eff": round(base / worst / n, 3),
+                          "host_enqueue_ms": round(max(host_ms), 3),
                           "ms_per_rank": [round(x, 3) for x in per_rank]}), flush=True)
 
 
