@@ -826,180 +826,200 @@ __device__ __forceinline__ const DevEmitter *select_emitter(const DeviceScene &s
     return e;
 }
 
+// One path that hit a surface of material MAT (0 = unknown type): emission and
+// MIS at the hit, loop head, NEE sample, BSDF sample (main.cu:84-163).
+// Returns the next/shadow flags byte (bit 0 extension ray, bit 1 shadow ray).
 template <uint32_t MAT>
-__global__ __launch_bounds__(kShadeBlock) void k_shade(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
-                                                       uint32_t bounce) {
-    const uint32_t bin = MAT == 0u ? 8u : MAT;
-    const uint32_t count = q.counts[bin];
-    const uint32_t *queue = q.bins + q.counts[kStartBins + bin];
-    const uint32_t stride = gridDim.x * blockDim.x;
-    const uint32_t wave_base = (blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
-    for (uint32_t base = wave_base; base < count; base += stride) {
-        const uint32_t i = base + lane_id();
-        const bool valid = i < count;
-        bool push_next = false, push_shadow = false;
-        uint32_t p = 0;
-        if (valid) {
-            p = queue[i];
-            const uint32_t s = p / fp.num_local;
-            const uint32_t l = p - s * fp.num_local;
-            const float4 h = ps.hit[p];
-            const float4 o4 = ps.ray_o[p];
-            const float4 d4 = ps.ray_d[p];
-            const vec3 ray_o = f3(o4), ray_d = f3(d4);
-            uint4 misc = ps.misc[p];
-            uint32_t rng = misc.x;
-            const uint32_t flags = misc.y;
-            float4 thr4 = ps.thr[p];
-            vec3 T = f3(thr4);
-            const float prev_pdf = thr4.w;
-            float4 rad4 = ps.rad[p];
-            vec3 L = f3(rad4);
-            const vec2 stale_uv = v2(__uint_as_float(misc.z), __uint_as_float(misc.w));
+__device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
+                                              uint32_t p, uint32_t bounce) {
+    bool push_next = false, push_shadow = false;
+    const uint32_t s = p / fp.num_local;
+    const uint32_t l = p - s * fp.num_local;
+    const float4 h = ps.hit[p];
+    const float4 o4 = ps.ray_o[p];
+    const float4 d4 = ps.ray_d[p];
+    const vec3 ray_o = f3(o4), ray_d = f3(d4);
+    uint4 misc = ps.misc[p];
+    uint32_t rng = misc.x;
+    const uint32_t flags = misc.y;
+    float4 thr4 = ps.thr[p];
+    vec3 T = f3(thr4);
+    const float prev_pdf = thr4.w;
+    float4 rad4 = ps.rad[p];
+    vec3 L = f3(rad4);
+    const vec2 stale_uv = v2(__uint_as_float(misc.z), __uint_as_float(misc.w));
 
-            HitGeo hg = reconstruct(sc, h, ray_o, ray_d, stale_uv);
-            const DevInstance &in = sc.instances[hg.inst];
-            const DevMaterial &mat = sc.materials[in.material];
-            if (mat.twosided && dot(-ray_d, hg.g.normal) < 0.f) hg.g.normal = -hg.g.normal;  // geometry.h:316-320
-            const LocalGeo &geo = hg.g;
-            LocalBsdf bsdf = local_bsdf(mat, geo.texcoord);
-            bsdf.type = MAT;
+    HitGeo hg = reconstruct(sc, h, ray_o, ray_d, stale_uv);
+    const DevInstance &in = sc.instances[hg.inst];
+    const DevMaterial &mat = sc.materials[in.material];
+    if (mat.twosided && dot(-ray_d, hg.g.normal) < 0.f) hg.g.normal = -hg.g.normal;  // geometry.h:316-320
+    const LocalGeo &geo = hg.g;
+    LocalBsdf bsdf = local_bsdf(mat, geo.texcoord);
+    bsdf.type = MAT;
 
-            bool alive = true;
-            if (bounce == 0) {
-                if (hg.emitter >= 0) L = L + emitter_radiance(sc.areas[hg.emitter], geo.texcoord);  // main.cu:88-92
-                const float test = rng_next(rng);                                                    // main.cu:101
-                if (s + 1 == fp.spp) {
-                    const uint32_t out = fp.compact ? l : global_pixel(fp, l);
-                    if (fp.albedo) {
-                        const vec3 al = bsdf_albedo(bsdf);
-                        fp.albedo[3 * out + 0] = al.x;
-                        fp.albedo[3 * out + 1] = al.y;
-                        fp.albedo[3 * out + 2] = al.z;
-                    }
-                    if (fp.normal) {
-                        fp.normal[3 * out + 0] = geo.normal.x;
-                        fp.normal[3 * out + 1] = geo.normal.y;
-                        fp.normal[3 * out + 2] = geo.normal.z;
-                    }
-                    if (fp.test) fp.test[out] = test;
-                }
-            } else if (hg.emitter >= 0) {  // main.cu:171-182
-                const DevEmitter &e = sc.areas[hg.emitter];
-                vec3 Le;
-                float pdf_e;
-                emitter_eval_area(e, geo, ray_o, Le, pdf_e);
-                if (!is_zero(pdf_e)) {
-                    const float mis = (flags >> 8) & 1u ? 1.f : mis_weight(prev_pdf, pdf_e * e.select_probability);
-                    L = L + T * Le * mis;
-                }
+    bool alive = true;
+    if (bounce == 0) {
+        if (hg.emitter >= 0) L = L + emitter_radiance(sc.areas[hg.emitter], geo.texcoord);  // main.cu:88-92
+        const float test = rng_next(rng);                                                    // main.cu:101
+        if (s + 1 == fp.spp) {
+            const uint32_t out = fp.compact ? l : global_pixel(fp, l);
+            if (fp.albedo) {
+                const vec3 al = bsdf_albedo(bsdf);
+                fp.albedo[3 * out + 0] = al.x;
+                fp.albedo[3 * out + 1] = al.y;
+                fp.albedo[3 * out + 2] = al.z;
             }
-
-            // loop head (main.cu:103-111)
-            const uint32_t depth = bounce + 1;
-            if (depth >= fp.max_depth) alive = false;
-            if (alive) {
-                const float rr = depth > 2 ? 0.95f : 1.0f;
-                if (rng_next(rng) > rr) alive = false;
-                else T = T / rr;
+            if (fp.normal) {
+                fp.normal[3 * out + 0] = geo.normal.x;
+                fp.normal[3 * out + 1] = geo.normal.y;
+                fp.normal[3 * out + 2] = geo.normal.z;
             }
-            float pdf_b = 0.f;
-            uint32_t delta = 0;
-            if (alive) {
-                // direct light sampling (main.cu:114-141)
-                float sel_prob;
-                const DevEmitter *e = select_emitter(sc, rng_next(rng), sel_prob);
-                const float x0 = rng_next(rng);
-                const float x1 = rng_next(rng);
-                const vec3 wo = to_local(-ray_d, geo.normal);
-                if (e) {
-                    const EmitterSample es = emitter_sample_direct(*e, geo, v2(x0, x1));
-                    BsdfRec er;
-                    er.wi = to_local(es.wi, geo.normal);
-                    er.wo = wo;
-                    er.f = v3(0.f);
-                    er.pdf = 0.f;
-                    bsdf_eval_t<MAT>(bsdf, er);
-                    if (!is_zero(er.f * es.pdf)) {
-                        const float NoL = dot(geo.normal, es.wi);
-                        if (NoL > 0.f) {
-                            const float mis = mis_weight(es.pdf, er.pdf);
-                            const float pdf_l = es.pdf * sel_prob;
-                            const vec3 C = T * es.radiance * er.f * NoL * mis / pdf_l;
-                            ps.sh_o[p] = f4(geo.position, es.distance - 0.001f);
-                            ps.sh_d[p] = f4(es.wi, 0.f);
-                            ps.sh_c[p] = f4(C, 0.f);
-                            push_shadow = true;
-                        }
-                    }
-                }
-                // BSDF sampling (main.cu:143-163)
-                BsdfRec br;
-                br.wo = wo;
-                br.wi = v3(0.f);
-                br.f = v3(0.f);
-                br.pdf = 0.f;
-                br.sampled_type = 0;
-                bsdf_sample_t<MAT>(bsdf, br, rng);
-                if (is_zero(br.f * fabs_(br.wi.z)) || is_zero(br.pdf)) {
-                    alive = false;
-                } else {
-                    T = T * (br.f * fabs_(br.wi.z) / br.pdf);
-                    const vec3 nd = to_world(br.wi, geo.normal);
-                    ps.ray_o[p] = f4(geo.position, 0.f);
-                    ps.ray_d[p] = f4(nd, 0.f);
-                    pdf_b = br.pdf;
-                    delta = (br.sampled_type & kLobeDelta) ? 1u : 0u;
-                    push_next = true;
-                }
-            }
-            ps.thr[p] = f4(T, pdf_b);
-            ps.rad[p] = f4(L, 0.f);
-            ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 8), __float_as_uint(geo.texcoord.x),
-                                    __float_as_uint(geo.texcoord.y));
+            if (fp.test) fp.test[out] = test;
         }
-        if (valid) ps.sflags[p] = (uint8_t)((push_next ? 1u : 0u) | (push_shadow ? 2u : 0u));
+    } else if (hg.emitter >= 0) {  // main.cu:171-182
+        const DevEmitter &e = sc.areas[hg.emitter];
+        vec3 Le;
+        float pdf_e;
+        emitter_eval_area(e, geo, ray_o, Le, pdf_e);
+        if (!is_zero(pdf_e)) {
+            const float mis = (flags >> 8) & 1u ? 1.f : mis_weight(prev_pdf, pdf_e * e.select_probability);
+            L = L + T * Le * mis;
+        }
     }
+
+    // loop head (main.cu:103-111)
+    const uint32_t depth = bounce + 1;
+    if (depth >= fp.max_depth) alive = false;
+    if (alive) {
+        const float rr = depth > 2 ? 0.95f : 1.0f;
+        if (rng_next(rng) > rr) alive = false;
+        else T = T / rr;
+    }
+    float pdf_b = 0.f;
+    uint32_t delta = 0;
+    if (alive) {
+        // direct light sampling (main.cu:114-141)
+        float sel_prob;
+        const DevEmitter *e = select_emitter(sc, rng_next(rng), sel_prob);
+        const float x0 = rng_next(rng);
+        const float x1 = rng_next(rng);
+        const vec3 wo = to_local(-ray_d, geo.normal);
+        if (e) {
+            const EmitterSample es = emitter_sample_direct(*e, geo, v2(x0, x1));
+            BsdfRec er;
+            er.wi = to_local(es.wi, geo.normal);
+            er.wo = wo;
+            er.f = v3(0.f);
+            er.pdf = 0.f;
+            bsdf_eval_t<MAT>(bsdf, er);
+            if (!is_zero(er.f * es.pdf)) {
+                const float NoL = dot(geo.normal, es.wi);
+                if (NoL > 0.f) {
+                    const float mis = mis_weight(es.pdf, er.pdf);
+                    const float pdf_l = es.pdf * sel_prob;
+                    const vec3 C = T * es.radiance * er.f * NoL * mis / pdf_l;
+                    ps.sh_o[p] = f4(geo.position, es.distance - 0.001f);
+                    ps.sh_d[p] = f4(es.wi, 0.f);
+                    ps.sh_c[p] = f4(C, 0.f);
+                    push_shadow = true;
+                }
+            }
+        }
+        // BSDF sampling (main.cu:143-163)
+        BsdfRec br;
+        br.wo = wo;
+        br.wi = v3(0.f);
+        br.f = v3(0.f);
+        br.pdf = 0.f;
+        br.sampled_type = 0;
+        bsdf_sample_t<MAT>(bsdf, br, rng);
+        if (is_zero(br.f * fabs_(br.wi.z)) || is_zero(br.pdf)) {
+            alive = false;
+        } else {
+            T = T * (br.f * fabs_(br.wi.z) / br.pdf);
+            const vec3 nd = to_world(br.wi, geo.normal);
+            ps.ray_o[p] = f4(geo.position, 0.f);
+            ps.ray_d[p] = f4(nd, 0.f);
+            pdf_b = br.pdf;
+            delta = (br.sampled_type & kLobeDelta) ? 1u : 0u;
+            push_next = true;
+        }
+    }
+    ps.thr[p] = f4(T, pdf_b);
+    ps.rad[p] = f4(L, 0.f);
+    ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 8), __float_as_uint(geo.texcoord.x),
+                            __float_as_uint(geo.texcoord.y));
+    return (push_next ? 1u : 0u) | (push_shadow ? 2u : 0u);
 }
 
 // Paths whose ray left the scene (__miss__default, main.cu:196-212, and the
 // env handling at main.cu:87-99 / 165-169).
-__global__ __launch_bounds__(kShadeBlock) void k_shade_miss(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
-                                                            uint32_t bounce) {
-    const uint32_t count = q.counts[0];
+__device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
+                                           uint32_t p, uint32_t bounce) {
+    if (bounce == 0) {
+        const uint32_t s = p / fp.num_local;
+        const uint32_t l = p - s * fp.num_local;
+        float4 rad4 = ps.rad[p];
+        vec3 L = f3(rad4);
+        uint32_t rng = ps.misc[p].x;
+        if (sc.has_env) {
+            vec3 Le;
+            float pdf;
+            env_eval(*sc.env, f3(ps.ray_o[p]), f3(ps.ray_d[p]), Le, pdf);
+            L = L + Le;  // main.cu:185, no MIS on the camera ray
+        }
+        const float test = rng_next(rng);
+        if (s + 1 == fp.spp) {
+            const uint32_t out = fp.compact ? l : global_pixel(fp, l);
+            if (fp.albedo) fp.albedo[3 * out] = fp.albedo[3 * out + 1] = fp.albedo[3 * out + 2] = 0.f;
+            if (fp.normal) fp.normal[3 * out] = fp.normal[3 * out + 1] = fp.normal[3 * out + 2] = 0.f;
+            if (fp.test) fp.test[out] = test;
+        }
+        ps.rad[p] = f4(L, 0.f);
+    } else if (sc.has_env) {
+        const float4 thr4 = ps.thr[p];
+        vec3 Le;
+        float env_pdf;
+        env_eval(*sc.env, f3(ps.ray_o[p]), f3(ps.ray_d[p]), Le, env_pdf);
+        const float mis = mis_weight(thr4.w, env_pdf);  // main.cu:166-167
+        const vec3 env_rad = Le * (f3(thr4) * mis);
+        float4 rad4 = ps.rad[p];
+        ps.rad[p] = f4(f3(rad4) + env_rad, 0.f);  // main.cu:185
+    }
+}
+
+// All shading of a bounce in one launch.  The material bins lie back to back in
+// q.bins (bin 0 = miss, 1..7 = EMatType, 8 = unknown type), each in increasing
+// path order, so a wave sees one material except at the 8 bin boundaries; the
+// branch below is wave-uniform almost everywhere.  One launch instead of nine
+// per bounce keeps empty-bin launches off the frame (they cost ~4 us each).
+__global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
+                                                           uint32_t bounce) {
+    const uint32_t count = q.counts[kScratch];  // all traced paths (total of the bin partition)
+    uint32_t start[kPartMaxBins];
+#pragma unroll
+    for (int b = 0; b < kPartMaxBins; b++) start[b] = q.counts[kStartBins + b];
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
         const uint32_t p = q.bins[i];
-        if (bounce == 0) {
-            const uint32_t s = p / fp.num_local;
-            const uint32_t l = p - s * fp.num_local;
-            float4 rad4 = ps.rad[p];
-            vec3 L = f3(rad4);
-            uint32_t rng = ps.misc[p].x;
-            if (sc.has_env) {
-                vec3 Le;
-                float pdf;
-                env_eval(*sc.env, f3(ps.ray_o[p]), f3(ps.ray_d[p]), Le, pdf);
-                L = L + Le;  // main.cu:185, no MIS on the camera ray
-            }
-            const float test = rng_next(rng);
-            if (s + 1 == fp.spp) {
-                const uint32_t out = fp.compact ? l : global_pixel(fp, l);
-                if (fp.albedo) fp.albedo[3 * out] = fp.albedo[3 * out + 1] = fp.albedo[3 * out + 2] = 0.f;
-                if (fp.normal) fp.normal[3 * out] = fp.normal[3 * out + 1] = fp.normal[3 * out + 2] = 0.f;
-                if (fp.test) fp.test[out] = test;
-            }
-            ps.rad[p] = f4(L, 0.f);
-        } else if (sc.has_env) {
-            const float4 thr4 = ps.thr[p];
-            vec3 Le;
-            float env_pdf;
-            env_eval(*sc.env, f3(ps.ray_o[p]), f3(ps.ray_d[p]), Le, env_pdf);
-            const float mis = mis_weight(thr4.w, env_pdf);  // main.cu:166-167
-            const vec3 env_rad = Le * (f3(thr4) * mis);
-            float4 rad4 = ps.rad[p];
-            ps.rad[p] = f4(f3(rad4) + env_rad, 0.f);  // main.cu:185
+        // bin of list position i: the last bin starting at or before i (an empty
+        // bin starts where the next one does, so it is never the last such bin)
+        uint32_t bin = 0;
+#pragma unroll
+        for (int b = 1; b < kPartMaxBins; b++) bin = i >= start[b] ? (uint32_t)b : bin;
+        uint32_t flags = 0;
+        switch (bin) {
+        case 0: shade_miss(sc, fp, ps, p, bounce); break;
+        case PUPIL_MAT_DIFFUSE: flags = shade_hit<PUPIL_MAT_DIFFUSE>(sc, fp, ps, p, bounce); break;
+        case PUPIL_MAT_DIELECTRIC: flags = shade_hit<PUPIL_MAT_DIELECTRIC>(sc, fp, ps, p, bounce); break;
+        case PUPIL_MAT_ROUGH_DIELECTRIC: flags = shade_hit<PUPIL_MAT_ROUGH_DIELECTRIC>(sc, fp, ps, p, bounce); break;
+        case PUPIL_MAT_CONDUCTOR: flags = shade_hit<PUPIL_MAT_CONDUCTOR>(sc, fp, ps, p, bounce); break;
+        case PUPIL_MAT_ROUGH_CONDUCTOR: flags = shade_hit<PUPIL_MAT_ROUGH_CONDUCTOR>(sc, fp, ps, p, bounce); break;
+        case PUPIL_MAT_PLASTIC: flags = shade_hit<PUPIL_MAT_PLASTIC>(sc, fp, ps, p, bounce); break;
+        case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p, bounce); break;
+        default: flags = shade_hit<0u>(sc, fp, ps, p, bounce); break;
         }
+        ps.sflags[p] = (uint8_t)flags;
     }
 }
 
@@ -1176,19 +1196,7 @@ void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues
 
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,
                   uint32_t bounce, hipStream_t s) {
-    const uint32_t blocks = 256u * 8u;
-    hipLaunchKernelGGL(k_shade_miss, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
-    hipLaunchKernelGGL(k_shade<PUPIL_MAT_DIFFUSE>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
-    hipLaunchKernelGGL(k_shade<PUPIL_MAT_DIELECTRIC>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
-    hipLaunchKernelGGL(k_shade<PUPIL_MAT_ROUGH_DIELECTRIC>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q,
-                       bounce);
-    hipLaunchKernelGGL(k_shade<PUPIL_MAT_CONDUCTOR>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
-    hipLaunchKernelGGL(k_shade<PUPIL_MAT_ROUGH_CONDUCTOR>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q,
-                       bounce);
-    hipLaunchKernelGGL(k_shade<PUPIL_MAT_PLASTIC>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
-    hipLaunchKernelGGL(k_shade<PUPIL_MAT_ROUGH_PLASTIC>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q,
-                       bounce);
-    hipLaunchKernelGGL(k_shade<0u>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
+    hipLaunchKernelGGL(k_shade_all, dim3(256u * 8u), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
 }
 
 void launch_accumulate(const FrameParams &fp, const PathState &ps, hipStream_t s) {

@@ -82,50 +82,76 @@ __global__ __launch_bounds__(kPartBlock) void k_part_count(const uint8_t *keys, 
 }
 
 // Exclusive scan of m = nbins * nblk entries in one block of 1024 threads.
+// The histogram streams through LDS in chunks of kScanChunk entries: coalesced
+// loads, a serial scan of 16 consecutive entries per thread in LDS, a block
+// scan of the per-thread sums, coalesced stores (the scan sits between two
+// full-chip kernels, so its latency is on the frame's critical path).
+constexpr uint32_t kScanPer = 16;
+constexpr uint32_t kScanChunk = 1024u * kScanPer;
+
 __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nblk, uint32_t nbins,
                                                     uint32_t *counts_out, uint32_t *starts_out,
                                                     uint32_t *total_out) {
+    __shared__ uint32_t sh[kScanChunk];
     __shared__ uint32_t wave_sum[16];
-    __shared__ uint32_t total;
+    __shared__ uint32_t carry_s;
     const uint32_t m = nbins * nblk;
     const uint32_t t = threadIdx.x;
-    const uint32_t per = (m + 1023u) / 1024u;
-    const uint32_t beg = min(t * per, m), end = min(beg + per, m);
-    uint32_t sum = 0;
-    for (uint32_t i = beg; i < end; i++) sum += hist[i];
-    // inclusive wave scan
-    uint32_t inc = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(inc, o);
-        if ((int)__lane_id() >= o) inc += v;
-    }
-    if (__lane_id() == 63) wave_sum[t >> 6] = inc;
-    __syncthreads();
-    if (t < 64) {
-        uint32_t w = t < 16 ? wave_sum[t] : 0u;
-        uint32_t winc = w;
-        for (int o = 1; o < 16; o <<= 1) {
-            const uint32_t v = __shfl_up(winc, o);
-            if ((int)t >= o) winc += v;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < m; c0 += kScanChunk) {
+        const uint32_t len = min(kScanChunk, m - c0);
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) {
+            const uint32_t i = k * 1024u + t;
+            sh[i] = i < len ? hist[c0 + i] : 0u;
         }
-        if (t < 16) wave_sum[t] = winc - w;  // exclusive wave offsets
-        if (t == 15) total = winc;
+        __syncthreads();
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) sum += sh[t * kScanPer + k];
+        uint32_t inc = sum;  // inclusive wave scan of the per-thread sums
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(inc, o);
+            if ((int)__lane_id() >= o) inc += v;
+        }
+        if (__lane_id() == 63) wave_sum[t >> 6] = inc;
+        __syncthreads();
+        if (t < 64) {
+            const uint32_t w = t < 16 ? wave_sum[t] : 0u;
+            uint32_t winc = w;
+            for (int o = 1; o < 16; o <<= 1) {
+                const uint32_t v = __shfl_up(winc, o);
+                if ((int)t >= o) winc += v;
+            }
+            if (t < 16) wave_sum[t] = winc - w;  // exclusive wave offsets
+            if (t == 15) carry_s = winc;         // chunk total
+        }
+        __syncthreads();
+        uint32_t run = carry + wave_sum[t >> 6] + inc - sum;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) {
+            const uint32_t v = sh[t * kScanPer + k];
+            sh[t * kScanPer + k] = run;
+            run += v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) {
+            const uint32_t i = k * 1024u + t;
+            if (i < len) hist[c0 + i] = sh[i];
+        }
+        carry += carry_s;
+        __syncthreads();
     }
-    __syncthreads();
-    uint32_t run = wave_sum[t >> 6] + inc - sum;
-    for (uint32_t i = beg; i < end; i++) {
-        const uint32_t v = hist[i];
-        hist[i] = run;
-        run += v;
-    }
+    __threadfence_block();
     __syncthreads();
     if (t < nbins) {
         const uint32_t start = hist[t * nblk];
-        const uint32_t next = t + 1 < nbins ? hist[(t + 1) * nblk] : total;
+        const uint32_t next = t + 1 < nbins ? hist[(t + 1) * nblk] : carry;
         starts_out[t] = start;
         counts_out[t] = next - start;
     }
-    if (t == 0 && total_out) *total_out = total;
+    if (t == 0 && total_out) *total_out = carry;
 }
 
 template <int MODE>
