@@ -500,7 +500,8 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     // traversal overflow stacks, counters, events
     pt->ovf_threads = trace_grid_blocks() * (uint32_t)kTraceBlock;
     if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 16) ||
-        pt->alloc(&pt->ray_log, 2 * 130) || pt->alloc(&pt->q.counts, kCountSlots))
+        pt->alloc(&pt->ray_log, 2 * 130) || pt->alloc(&pt->q.counts, kCountSlots) ||
+        pt->alloc(&pt->q.work, kWorkSlots))
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
@@ -647,13 +648,14 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     };
     launch_generate(pt->sc, fp, pt->ps, s);
     HIP_TRY(hipMemsetAsync(q.counts, 0, kCountSlots * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(q.work, 0, kWorkSlots * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(pt->ps.mbin, 0xFF, np, s));
     ev0(0);
     launch_extend(pt->sc, pt->ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s);
     ev1();
     bin_paths();
     for (uint32_t b = 0; b < bounces; b++) {
-        HIP_TRY(hipMemsetAsync(q.counts + kWorkExtend, 0, 3 * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(q.work, 0, kWorkSlots * sizeof(uint32_t), s));
         HIP_TRY(hipMemsetAsync(pt->ps.sflags, 0, np, s));
         ev0(2);
         launch_shade(pt->sc, fp, pt->ps, q, b, s);
@@ -764,9 +766,9 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
     hipError_t e = hipMalloc((void **)&d_out, sizeof(float) * 4 * (size_t)n);
     if (e == hipSuccess) e = hipMemcpy(d_rays, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        e = hipMemsetAsync(pt->q.counts + kWorkRays, 0, sizeof(uint32_t), pt->own_stream);
+        e = hipMemsetAsync(pt->q.work + kWorkRays, 0, kWorkShards * kWorkStride * sizeof(uint32_t), pt->own_stream);
         if (e == hipSuccess)
-            launch_trace_debug(pt->sc, d_rays, d_out, n, any_hit, pt->ovf, pt->ovf_threads, pt->q.counts + kWorkRays,
+            launch_trace_debug(pt->sc, d_rays, d_out, n, any_hit, pt->ovf, pt->ovf_threads, pt->q.work + kWorkRays,
                                pt->own_stream);
         e = hipStreamSynchronize(pt->own_stream);
     }

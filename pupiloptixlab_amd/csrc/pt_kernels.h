@@ -37,7 +37,10 @@ struct PathState {
 constexpr int kPartMaxBins = 9;
 // counts[] slots
 constexpr uint32_t kCntNext = 9, kCntShadow = 10;                      // queue lengths
-constexpr uint32_t kWorkExtend = 11, kWorkShadow = 12, kWorkRays = 13;  // persistent-kernel work counters
+// persistent-kernel work counters: kWorkShards heads per kind (one per XCD), each on its own 128-B line
+constexpr uint32_t kWorkShards = 8, kWorkStride = 32;
+constexpr uint32_t kWorkExtend = 0, kWorkShadow = kWorkShards * kWorkStride, kWorkRays = 2 * kWorkShards * kWorkStride;
+constexpr uint32_t kWorkSlots = 3 * kWorkShards * kWorkStride;
 constexpr uint32_t kStartBins = 16;                                    // [16..24] material bin starts
 constexpr uint32_t kStartNext = 25, kStartShadow = 26;                 // next / shadow regions of nxsh
 constexpr uint32_t kScratch = 27;
@@ -48,6 +51,7 @@ struct Queues {
     uint32_t *nxsh;      // 2 * capacity: next ids from counts[kStartNext] (= 0), shadow ids from counts[kStartShadow]
     uint32_t *counts;    // kCountSlots entries, see above
     uint32_t *hist;      // partition scratch, partition_hist_entries(capacity)
+    uint32_t *work;      // kWorkSlots persistent-kernel work heads (see kWorkExtend)
     uint32_t capacity;
 };
 

@@ -447,7 +447,7 @@ struct TraceJob {
     const uint32_t *queue;      // extend: path ids (null = identity)
     const uint32_t *count_ptr;  // device count (null = static_count)
     uint32_t static_count;
-    uint32_t *work;             // work counter, zero at launch
+    uint32_t *work;             // kWorkShards work heads (stride kWorkStride), zero at launch
     uint32_t refill;            // refill when at least this many lanes are idle (1..64)
     uint32_t node_min;          // node phase ends when fewer lanes than this still need a node (>= 1)
     const float *rays;          // kModeRays: 8 floats per ray (o, d, tmin, tmax)
@@ -549,6 +549,13 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     // lanes, refills / lanes refilled
     unsigned long long dg[6] = {0, 0, 0, 0, 0, 0};
     bool active = false, drained = false;
+    // XCD-sharded dequeue (one atomic head per XCD: a single head saturates at
+    // ~88 dequeues/us, MI355X_MICROARCH.md 'dequeue', which is the refill rate
+    // of this kernel).  The work list is cut into kWorkShards contiguous chunks;
+    // workgroups start on chunk blockIdx % kWorkShards (the dispatcher deals
+    // workgroups round-robin over the XCDs) and move on to the next chunk when
+    // theirs is exhausted, so every item is taken exactly once.
+    uint32_t shard = blockIdx.x % kWorkShards, tried = 0;
     uint32_t p = 0, best_key = 0, best_idx = kMissIndex;
     RayPre r{};
     float tmin = 0.f, tmax = 0.f, b1 = 0.f, b2 = 0.f;
@@ -560,17 +567,23 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
         const unsigned long long idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
         if (!drained && n_idle >= job.refill) {
+            const uint32_t lo = (uint32_t)((uint64_t)count * shard / kWorkShards);
+            const uint32_t len = (uint32_t)((uint64_t)count * (shard + 1) / kWorkShards) - lo;
             uint32_t base = 0;
-            if (lane_id() == 0) base = atomicAdd(job.work, n_idle);
+            if (lane_id() == 0) base = atomicAdd(job.work + shard * kWorkStride, n_idle);
             base = __shfl(base, 0);
             if (STATS && lane_id() == 0) {
                 dg[4]++;
-                dg[5] += min(n_idle, base < count ? count - base : 0u);
+                dg[5] += min(n_idle, base < len ? len - base : 0u);
             }
-            if (base + n_idle >= count) drained = true;
+            if (base + n_idle >= len) {  // chunk exhausted: continue on the next one
+                shard = shard + 1 == kWorkShards ? 0u : shard + 1;
+                if (++tried == kWorkShards) drained = true;
+            }
             if (!active) {
-                const uint32_t i = base + (uint32_t)__popcll(idle & lanemask_lt());
-                if (i < count) {
+                const uint32_t k = base + (uint32_t)__popcll(idle & lanemask_lt());
+                const uint32_t i = lo + k;
+                if (k < len) {
                     float4 o, d;
                     if (MODE == kModeExtend) {
                         p = job.queue ? job.queue[i] : i;
@@ -1130,7 +1143,7 @@ void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
     if (w4 && sc.trace_refill) {
-        const TraceJob job{queue, queue_count, static_count, q.counts + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
+        const TraceJob job{queue, queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
         if (stats)
             hipLaunchKernelGGL((k_trace4<kModeExtend, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
@@ -1159,7 +1172,7 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
     if (w4 && sc.trace_refill) {
-        const TraceJob job{nullptr, nullptr, 0u, q.counts + kWorkShadow, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
+        const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkShadow, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
         if (stats)
             hipLaunchKernelGGL((k_trace4<kModeShadow, true, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
@@ -1184,7 +1197,7 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                         const TraceStats *stats, hipStream_t s) {
     TraceStats st = stats ? *stats : TraceStats{nullptr};
-    const TraceJob job{nullptr, nullptr, 0u, q.counts + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
+    const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
     const uint32_t blocks = trace4_blocks(sc, ovf_threads);
     if (stats)
         hipLaunchKernelGGL((k_trace4<kModeMixed, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,

@@ -47,7 +47,6 @@ def main():
                 h0 = time.perf_counter()
                 pt.render(8, stream=s)
                 host += time.perf_counter() - h0
-                pt.stats()
             torch.cuda.synchronize()
             per_rank.append((time.perf_counter() - t0) / args.frames * 1e3)
             host_ms.append(host / args.frames * 1e3)
