@@ -486,7 +486,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pt->device);
     sc.num_cus = (uint32_t)std::max(1, cus);
-    sc.trace_refill = 40;  // persistent BVH4 kernels; 0 selects the one-ray-per-lane kernels (A/B)
+    sc.trace_refill = 24;  // persistent BVH4 kernels; 0 selects the one-ray-per-lane kernels (A/B)
     if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
@@ -503,6 +503,8 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         pt->alloc(&pt->ray_log, 2 * 130) || pt->alloc(&pt->q.counts, kCountSlots) ||
         pt->alloc(&pt->q.work, kWorkSlots))
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
+    if (hipMemset(pt->q.work, 0, kWorkSlots * sizeof(uint32_t)) != hipSuccess)
+        return cleanup(fail(PUPIL_ERR_HIP, "workspace clear failed"));
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
     pt->totals.bvh_nodes = pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes;
@@ -638,38 +640,34 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
 
     HIP_TRY(hipEventRecord(pt->ev_begin, s));
     if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 16 * sizeof(unsigned long long), s));
-    HIP_TRY(hipMemsetAsync(pt->ray_log, 0, sizeof(uint32_t) * 2 * 130, s));
     const uint32_t np = fp.num_paths;
     Queues &q = pt->q;
     // material bins of the traced paths -> q.bins (stable, increasing path id)
     auto bin_paths = [&]() {
         launch_partition(pt->ps.mbin, np, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
-                         q.counts + kStartBins, q.counts + kScratch, s);
+                         q.counts + kStartBins, q.counts + kScratch, nullptr, s);
     };
+    // No per-stage clears: the primary extend writes every path's material bin,
+    // each shade writes its paths' flags (with the bounce tag) and resets their
+    // bin to 0xFF, the persistent kernels reset their own work heads, and the
+    // flags partition logs the per-bounce ray counts.
     launch_generate(pt->sc, fp, pt->ps, s);
-    HIP_TRY(hipMemsetAsync(q.counts, 0, kCountSlots * sizeof(uint32_t), s));
-    HIP_TRY(hipMemsetAsync(q.work, 0, kWorkSlots * sizeof(uint32_t), s));
-    HIP_TRY(hipMemsetAsync(pt->ps.mbin, 0xFF, np, s));
     ev0(0);
     launch_extend(pt->sc, pt->ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s);
     ev1();
     bin_paths();
     for (uint32_t b = 0; b < bounces; b++) {
-        HIP_TRY(hipMemsetAsync(q.work, 0, kWorkSlots * sizeof(uint32_t), s));
-        HIP_TRY(hipMemsetAsync(pt->ps.sflags, 0, np, s));
+        const uint32_t tag = sflag_tag(fp.max_depth, b);
+        if (tag == 0) HIP_TRY(hipMemsetAsync(pt->ps.sflags, 0, np, s));
         ev0(2);
         launch_shade(pt->sc, fp, pt->ps, q, b, s);
         ev1();
         if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
             // next (bit 0) and shadow (bit 1) lists -> q.nxsh, each in increasing path order
             // (grouping the next list by direction octant measured slower: 21.2 vs 20.8 ms extend)
-            launch_partition(pt->ps.sflags, np, 2, kPartFlags, 0u, q.nxsh, q.hist, q.counts + kCntNext,
-                             q.counts + kStartNext, nullptr, s);
-            if (b < 128)
-                HIP_TRY(hipMemcpyAsync(pt->ray_log + 2 * b, q.counts + kCntNext, 2 * sizeof(uint32_t),
-                                       hipMemcpyDeviceToDevice, s));
+            launch_partition(pt->ps.sflags, np, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
+                             q.counts + kStartNext, nullptr, b < 128 ? pt->ray_log + 2 * b : nullptr, s);
             if (pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill) {
-                HIP_TRY(hipMemsetAsync(pt->ps.mbin, 0xFF, np, s));
                 ev0(1);
                 launch_trace_mixed(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);
                 ev1();
@@ -677,7 +675,6 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
                 ev0(1);
                 launch_shadow(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);
                 ev1();
-                HIP_TRY(hipMemsetAsync(pt->ps.mbin, 0xFF, np, s));
                 ev0(0);
                 launch_extend(pt->sc, pt->ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, tsp, s);
                 ev1();
@@ -690,7 +687,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     HIP_TRY(hipGetLastError());
     pt->trace_pairs = pair;
     pt->last_paths = fp.num_paths;
-    pt->last_bounces = bounces < 128 ? bounces : 128;
+    pt->last_bounces = bounces < 129 ? bounces : 129;  // rays are logged for bounces 0..127
     pt->last_stats = stats;
     return PUPIL_OK;
 }
@@ -707,7 +704,7 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
         c.path_samples = pt->last_paths;
         c.extension_rays = 0;
         c.shadow_rays = 0;
-        for (uint32_t b = 0; b < pt->last_bounces; b++) {
+        for (uint32_t b = 0; b + 1 < pt->last_bounces; b++) {  // the last bounce spawns no rays
             c.extension_rays += log[2 * b];
             c.shadow_rays += log[2 * b + 1];
         }

@@ -29,18 +29,28 @@ struct PathState {
     float4 *sh_d;       // shadow ray direction
     float4 *sh_c;       // pending NEE contribution
     uint8_t *mbin;      // extend -> material bin of the hit (0 miss, 1..7 EMatType, 8 unknown), 0xFF = not traced
-    uint8_t *sflags;    // shade -> bit 0: extension ray spawned, bit 1: shadow ray spawned
+    uint8_t *sflags;    // shade -> bit 0: extension ray spawned, bit 1: shadow ray spawned, bits 2..7: bounce tag
 };
+
+// Bounce tag of the shade flags byte: the flags partition after bounce b lists
+// only bytes carrying tag(b), so the flags a path left when it died are never
+// listed again and no per-bounce clear is needed.  Depths above 63 would alias
+// the 6-bit tag: there the tag is 0 and the engine clears the bytes per bounce.
+__host__ __device__ inline uint32_t sflag_tag(uint32_t max_depth, uint32_t bounce) {
+    return max_depth <= 63u ? bounce % 63u + 1u : 0u;
+}
 
 // Queues are rebuilt by a stable partition (queue_partition.hip) after each
 // stage, so every queue lists path ids in increasing order.
 constexpr int kPartMaxBins = 9;
 // counts[] slots
 constexpr uint32_t kCntNext = 9, kCntShadow = 10;                      // queue lengths
-// persistent-kernel work counters: kWorkShards heads per kind (one per XCD), each on its own 128-B line
-constexpr uint32_t kWorkShards = 8, kWorkStride = 32;
-constexpr uint32_t kWorkExtend = 0, kWorkShadow = kWorkShards * kWorkStride, kWorkRays = 2 * kWorkShards * kWorkStride;
-constexpr uint32_t kWorkSlots = 3 * kWorkShards * kWorkStride;
+// persistent-kernel work counters: per kind kWorkShards dequeue heads (one per
+// XCD) and one exit counter, each on its own 128-B line.  Zero at allocation;
+// the last wave of every persistent launch puts them back to zero.
+constexpr uint32_t kWorkShards = 8, kWorkStride = 32, kWorkKind = (kWorkShards + 1) * kWorkStride;
+constexpr uint32_t kWorkExtend = 0, kWorkShadow = kWorkKind, kWorkRays = 2 * kWorkKind;
+constexpr uint32_t kWorkSlots = 3 * kWorkKind;
 constexpr uint32_t kStartBins = 16;                                    // [16..24] material bin starts
 constexpr uint32_t kStartNext = 25, kStartShadow = 26;                 // next / shadow regions of nxsh
 constexpr uint32_t kScratch = 27;
@@ -58,7 +68,7 @@ struct Queues {
 // partition key modes (queue_partition.hip)
 enum PartMode : int {
     kPartExclusive = 0,  // bin = key >> shift (0xFF = none)
-    kPartFlags = 1,      // bin b <=> bit (shift + b) of the key
+    kPartFlags = 1,      // bin b <=> bit b of the key, if key >> 2 == tag (passed as `shift`)
 };
 
 struct FrameParams {
@@ -104,7 +114,8 @@ void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, 
 // stable partition of path ids 0..n-1 by a key byte (queue_partition.hip)
 uint32_t partition_hist_entries(uint32_t n);
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
-                      uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, hipStream_t s);
+                      uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, uint32_t *log_out,
+                      hipStream_t s);
 
 // LBVH builder (bvh_build.hip)
 struct BvhBuildInput {

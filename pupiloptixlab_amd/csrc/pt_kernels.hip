@@ -447,7 +447,7 @@ struct TraceJob {
     const uint32_t *queue;      // extend: path ids (null = identity)
     const uint32_t *count_ptr;  // device count (null = static_count)
     uint32_t static_count;
-    uint32_t *work;             // kWorkShards work heads (stride kWorkStride), zero at launch
+    uint32_t *work;             // kWorkShards work heads + exit counter (stride kWorkStride), zero at launch
     uint32_t refill;            // refill when at least this many lanes are idle (1..64)
     uint32_t node_min;          // node phase ends when fewer lanes than this still need a node (>= 1)
     const float *rays;          // kModeRays: 8 floats per ray (o, d, tmin, tmax)
@@ -712,6 +712,12 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     }
     flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
     if (MODE == kModeMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
+    // the last wave out resets the heads for the next launch (no memset per launch)
+    if (lane_id() == 0) {
+        const uint32_t waves = gridDim.x * (blockDim.x / 64u);
+        if (atomicAdd(job.work + kWorkShards * kWorkStride, 1u) == waves - 1u)
+            for (uint32_t k = 0; k <= kWorkShards; k++) atomicExch(job.work + k * kWorkStride, 0u);
+    }
     if (STATS) {
         for (int k = 0; k < 6; k++) {
             unsigned long long v = dg[k];
@@ -1009,6 +1015,7 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
 __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
                                                            uint32_t bounce) {
     const uint32_t count = q.counts[kScratch];  // all traced paths (total of the bin partition)
+    const uint32_t tag = sflag_tag(fp.max_depth, bounce);
     uint32_t start[kPartMaxBins];
 #pragma unroll
     for (int b = 0; b < kPartMaxBins; b++) start[b] = q.counts[kStartBins + b];
@@ -1032,7 +1039,8 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, Frame
         case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p, bounce); break;
         default: flags = shade_hit<0u>(sc, fp, ps, p, bounce); break;
         }
-        ps.sflags[p] = (uint8_t)flags;
+        ps.sflags[p] = (uint8_t)(flags | tag << 2);
+        ps.mbin[p] = 0xFFu;  // listed again only if the next extend traces this path
     }
 }
 

@@ -16,7 +16,8 @@
 //   k_part_scatter  per tile: recount per wave, then rank with ballots and write
 //
 // Modes (PartMode, pt_kernels.h): exclusive (bin = key >> shift, 0xFF none),
-// flags (bit shift + b puts the path in bin b; a path can be in several).
+// flags (bit b puts the path in bin b when the key's bounce tag, bits 2..7,
+// equals `shift`; a path can be in several bins).
 #include <algorithm>
 
 #include "pt_kernels.h"
@@ -47,7 +48,7 @@ __device__ __forceinline__ uint32_t no_key() {
 template <int MODE>
 __device__ __forceinline__ bool in_bin(uint32_t k, uint32_t b, uint32_t shift) {
     if (MODE == kPartExclusive) return (k >> shift) == b && k != 0xFFu;
-    return ((k >> (shift + b)) & 1u) != 0u;  // kPartFlags
+    return ((k >> b) & 1u) != 0u && (k >> 2) == shift;  // kPartFlags: shift carries the bounce tag
 }
 
 __device__ __forceinline__ unsigned long long lanes_below() { return (1ull << __lane_id()) - 1ull; }
@@ -91,7 +92,7 @@ constexpr uint32_t kScanChunk = 1024u * kScanPer;
 
 __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nblk, uint32_t nbins,
                                                     uint32_t *counts_out, uint32_t *starts_out,
-                                                    uint32_t *total_out) {
+                                                    uint32_t *total_out, uint32_t *log_out) {
     __shared__ uint32_t sh[kScanChunk];
     __shared__ uint32_t wave_sum[16];
     __shared__ uint32_t carry_s;
@@ -150,6 +151,7 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nbl
         const uint32_t next = t + 1 < nbins ? hist[(t + 1) * nblk] : carry;
         starts_out[t] = start;
         counts_out[t] = next - start;
+        if (log_out) log_out[t] = next - start;
     }
     if (t == 0 && total_out) *total_out = carry;
 }
@@ -196,20 +198,22 @@ uint32_t partition_hist_entries(uint32_t n) {
 }
 
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
-                      uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, hipStream_t s) {
+                      uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, uint32_t *log_out,
+                      hipStream_t s) {
     const uint32_t nblk = part_blocks(n);
     const uint32_t rounds = part_rounds(n);
     if (nblk == 0) {
         (void)hipMemsetAsync(counts_out, 0, sizeof(uint32_t) * nbins, s);
         (void)hipMemsetAsync(starts_out, 0, sizeof(uint32_t) * nbins, s);
         if (total_out) (void)hipMemsetAsync(total_out, 0, sizeof(uint32_t), s);
+        if (log_out) (void)hipMemsetAsync(log_out, 0, sizeof(uint32_t) * nbins, s);
         return;
     }
 #define PART_RUN(M)                                                                                                \
     hipLaunchKernelGGL(k_part_count<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk,      \
                        rounds);                                                                                    \
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, hist, nblk, nbins, counts_out, starts_out,          \
-                       total_out);                                                                                 \
+                       total_out, log_out);                                                                                 \
     hipLaunchKernelGGL(k_part_scatter<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk, out, \
                        rounds)
     switch (mode) {

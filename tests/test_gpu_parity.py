@@ -160,6 +160,17 @@ def test_stage_schedules_parity(mixed, monkeypatch):
         (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
 
 
+def test_deep_paths_parity():
+    """max_depth 70 > 63: the flags byte carries no bounce tag and is cleared every bounce."""
+    w = _cornell(48, depth=70)
+    desc = w.desc()
+    gpu = render_gpu(desc, 2)
+    ref = oracle.OracleScene(desc).render(spp=2)
+    assert compare(gpu, ref, "cornell48-depth70") == 48 * 48
+    s, rs = gpu["stats"], ref["stats"]
+    assert (s["extension_rays"], s["shadow_rays"]) == (rs["extension_rays"], rs["shadow_rays"])
+
+
 # (PUPIL_BVH_WIDTH, PUPIL_REFILL): BVH2, BVH4 one-ray-per-lane, BVH4 persistent with several refill thresholds
 TRAVERSALS = [("2", "16"), ("4", "0"), ("4", "1"), ("4", "16"), ("4", "64")]
 
