@@ -41,19 +41,26 @@ def load(root):
     return vals, dur
 
 
-def traffic_json(root, kernel, out_path, note=""):
-    """Per-launch L2->fabric bytes of one kernel: 2 x FETCH_SIZE (gfx950 half-count
-    correction for 16 B/lane loads) + WRITE_SIZE, both KiB in rocprofv3."""
+def traffic_json(root, kernels, out_path, note=""):
+    """Per-launch L2->fabric bytes of one kernel (or of several template
+    instances of it, "a|b", averaged over their dispatches): 2 x FETCH_SIZE
+    (gfx950 half-count correction for 16 B/lane loads) + WRITE_SIZE, both KiB
+    in rocprofv3."""
     import json
 
     vals, dur = load(root)
-    k = next(k for k in vals if k == kernel)
-    f = sum(vals[k]["FETCH_SIZE"]) / len(vals[k]["FETCH_SIZE"])
-    w = sum(vals[k]["WRITE_SIZE"]) / len(vals[k]["WRITE_SIZE"])
-    hit = sum(vals[k].get("TCC_HIT_sum", [0])) / max(1, len(vals[k].get("TCC_HIT_sum", [0])))
-    miss = sum(vals[k].get("TCC_MISS_sum", [0])) / max(1, len(vals[k].get("TCC_MISS_sum", [0])))
-    d = dur[k]
-    rec = {"kernel": k, "fetch_size_kib": f, "write_size_kib": w,
+    names = kernels.split("|")
+    ks = [k for k in vals if k in names]
+    assert ks, f"no kernel named {names} in {root}"
+
+    def pooled(c):
+        v = [x for k in ks for x in vals[k].get(c, [])]
+        return sum(v) / max(1, len(v))
+
+    f, w = pooled("FETCH_SIZE"), pooled("WRITE_SIZE")
+    hit, miss = pooled("TCC_HIT_sum"), pooled("TCC_MISS_sum")
+    d = [x for k in ks for x in dur[k]]
+    rec = {"kernel": " + ".join(ks), "fetch_size_kib": f, "write_size_kib": w,
            "traffic_bytes_per_launch": (2.0 * f + w) * 1024.0,
            "l2_hit_rate": hit / max(1.0, hit + miss),
            "avg_ms_under_pmc": sum(d) / len(d) / 1e6, "note": note}
