@@ -223,6 +223,7 @@ typedef struct pupil_pt_counters {
     uint64_t extend_prim_tests;
     double extend_bytes;
     double shade_ms;         /* device time of the shade stages (all materials) */
+    uint64_t two_level;      /* 1: TLAS over instances + per-shape BLAS; 0: one flattened BVH */
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;

@@ -1,0 +1,48 @@
+// accel_two_level.h — two-level acceleration structure (TLAS over instances,
+// one object-space BLAS per mesh shape); see accel_two_level.hip.
+#pragma once
+
+#include <vector>
+
+#include "pt_kernels.h"
+
+namespace pupil {
+
+struct TwoLevelShape {  // one mesh shape (device arrays, object space)
+    uint32_t num_faces, num_vertices;
+    const float *positions, *normals, *texcoords;
+    const uint32_t *indices;
+    float vmax;  // largest |coordinate| of its vertices (host-computed; for the box margin)
+};
+
+struct TwoLevelAccel {
+    Bvh4Node *nodes4 = nullptr;  // [0, tlas_cap) TLAS, then the rebased BLASes
+    float4 *prims = nullptr;     // 3 float4 per BLAS primitive, object space, BLAS leaf order; w of [0] = local id
+    float4 *attrs = nullptr;     // kAttrStride float4 per BLAS primitive, the mesh's own primitive order
+    float *d_boxes = nullptr;    // 6 floats per instance: world box
+    uint32_t *d_list = nullptr, *d_verts = nullptr;  // scratch: instance list, vertices per instance
+    uint32_t tlas_cap = 0, tlas_nodes = 0, num_nodes4 = 0, num_prims = 0;
+    uint32_t root_link4 = (uint32_t)kTraverseDone;
+    double build_ms = 0.0;
+};
+
+// Link of a node or leaf of one BLAS after it is copied to node_base / prim_base.
+PT_HD int rebase_link(int link, uint32_t node_base, uint32_t prim_base) {
+    if (link == kEmptyLink || link == kTraverseDone) return link;
+    if (link >= 0) return link + (int)node_base;
+    return make_leaf(leaf_first(link) + prim_base, leaf_count(link));
+}
+
+// Builds the BLASes, fills the two-level fields of every instance (host copy
+// `insts`, uploaded to d_insts), their world boxes and the TLAS.
+// inst_shape[i] = shape index of instance i (ignored for spheres).
+int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<uint32_t> &inst_shape,
+                    std::vector<DevInstance> &insts, DevInstance *d_insts, const DevMaterial *d_mats,
+                    uint32_t leaf_size, hipStream_t s, TwoLevelAccel &acc);
+// Recomputes the world boxes of the `changed` instances (transforms already in
+// insts / d_insts) and rebuilds the TLAS.
+int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstance *d_insts,
+                 const std::vector<uint32_t> &changed, hipStream_t s);
+void free_two_level(TwoLevelAccel &acc);
+
+}  // namespace pupil

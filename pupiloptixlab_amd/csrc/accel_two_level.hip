@@ -1,0 +1,387 @@
+// accel_two_level.hip — two-level acceleration structure (the reference's
+// IAS -> GAS hierarchy, world/ias_manager.cpp:29-114 + world/gas_manager.cpp:61-185).
+//
+// One object-space BLAS per mesh shape, built by the GPU builder
+// (bvh_build.hip, object_space mode: PLOC + greedy BVH4 collapse, 64 B
+// quantized nodes), and one TLAS over the instances whose leaves hold one
+// instance each.  All nodes live in one Bvh4Node array: the TLAS in
+// [0, tlas_cap), the BLASes after it with their links rebased.
+//
+// Hits stay bit-identical to the flattened single-level BVH and to the CPU
+// oracle: BLAS boxes are only used for culling (with a margin that covers the
+// object-space ray's rounding, see instance_margin), and every triangle is
+// tested in WORLD space on its world vertices fl(to_world * v), computed with
+// the same xform_point the flattened build and the oracle use.
+//
+// The TLAS is rebuilt on the host from the instance world boxes (binned SAH
+// over a few instances is microseconds); an instance update recomputes that
+// instance's box on the GPU and rebuilds the TLAS, the BLASes never change
+// (the reference refits its IAS, ias_manager.cpp:116-151).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "accel_two_level.h"
+#include "bvh4_quant.h"
+
+namespace pupil {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// World box of each listed instance: exact bounds of its world-space vertices
+// fl(to_world * v) (a mesh: every vertex; a sphere: the padded box of
+// bvh_build.hip k_prim_setup).  One block per instance.
+__global__ __launch_bounds__(kBlock) void k_inst_bounds(const DevInstance *insts, const uint32_t *list,
+                                                        const uint32_t *num_verts, float *out) {
+    __shared__ float red[kBlock / 64][6];
+    const uint32_t id = list[blockIdx.x];
+    const DevInstance &in = insts[id];
+    float *o = out + 6 * (size_t)id;
+    if (in.kind == PUPIL_SHAPE_SPHERE) {
+        if (threadIdx.x == 0) {
+            const float *m = in.to_world;
+            const float ex = sqrtf(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.0001f;
+            const float ey = sqrtf(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.0001f;
+            const float ez = sqrtf(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.0001f;
+            o[0] = m[3] - ex;
+            o[1] = m[7] - ey;
+            o[2] = m[11] - ez;
+            o[3] = m[3] + ex;
+            o[4] = m[7] + ey;
+            o[5] = m[11] + ez;
+        }
+        return;
+    }
+    float v[6] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf(),
+                  -__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+    const uint32_t nv = num_verts[id];
+    for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) {
+        const float *P = in.positions + 3 * (size_t)i;
+        const vec3 w = xform_point(in.to_world, v3(P[0], P[1], P[2]));
+        v[0] = fminf(v[0], w.x);
+        v[1] = fminf(v[1], w.y);
+        v[2] = fminf(v[2], w.z);
+        v[3] = fmaxf(v[3], w.x);
+        v[4] = fmaxf(v[4], w.y);
+        v[5] = fmaxf(v[5], w.z);
+    }
+    for (int s = 32; s > 0; s >>= 1)
+        for (int k = 0; k < 6; k++) {
+            const float x = __shfl_xor(v[k], s);
+            v[k] = k < 3 ? fminf(v[k], x) : fmaxf(v[k], x);
+        }
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 6; k++) red[threadIdx.x >> 6][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 6; k++) {
+            float x = red[0][k];
+            for (int w = 1; w < kBlock / 64; w++) x = k < 3 ? fminf(x, red[w][k]) : fmaxf(x, red[w][k]);
+            o[k] = x;
+        }
+}
+
+// Rebase the links of one BLAS copied into the combined node array.
+__global__ void k_relink(Bvh4Node *nodes, uint32_t count, uint32_t node_base, uint32_t prim_base) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    Bvh4Node &n = nodes[node_base + i];
+    for (int k = 0; k < 4; k++) n.child[k] = rebase_link(n.child[k], node_base, prim_base);
+}
+
+struct HostBox {
+    float lo[3], hi[3];
+    void grow(const HostBox &b) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
+        }
+    }
+    float area() const {
+        const float dx = std::max(0.f, hi[0] - lo[0]), dy = std::max(0.f, hi[1] - lo[1]),
+                    dz = std::max(0.f, hi[2] - lo[2]);
+        return dx * dy + dy * dz + dz * dx;
+    }
+    static HostBox empty() {
+        const float inf = __builtin_huge_valf();
+        return HostBox{{inf, inf, inf}, {-inf, -inf, -inf}};
+    }
+};
+
+// Top-down SAH split of ids[b, e) (centroid sort on the widest axis, sweep).
+uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std::vector<HostBox> &boxes) {
+    HostBox cb = HostBox::empty();
+    for (uint32_t i = b; i < e; i++) {
+        const HostBox &x = boxes[ids[i]];
+        for (int k = 0; k < 3; k++) {
+            const float c = 0.5f * (x.lo[k] + x.hi[k]);
+            cb.lo[k] = std::min(cb.lo[k], c);
+            cb.hi[k] = std::max(cb.hi[k], c);
+        }
+    }
+    int axis = 0;
+    for (int k = 1; k < 3; k++)
+        if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+    std::stable_sort(ids.begin() + b, ids.begin() + e, [&](uint32_t x, uint32_t y) {
+        return boxes[x].lo[axis] + boxes[x].hi[axis] < boxes[y].lo[axis] + boxes[y].hi[axis];
+    });
+    const uint32_t n = e - b;
+    std::vector<float> right(n + 1, 0.f);
+    HostBox acc = HostBox::empty();
+    for (uint32_t i = n; i-- > 1;) {
+        acc.grow(boxes[ids[b + i]]);
+        right[i] = acc.area() * (float)(n - i);
+    }
+    acc = HostBox::empty();
+    float best = __builtin_huge_valf();
+    uint32_t split = b + n / 2;
+    for (uint32_t i = 1; i < n; i++) {
+        acc.grow(boxes[ids[b + i - 1]]);
+        const float cost = acc.area() * (float)i + right[i];
+        if (cost < best) {
+            best = cost;
+            split = b + i;
+        }
+    }
+    return split;
+}
+
+// 4-wide TLAS node over ids[b, e) (two levels of binary SAH splits); returns its link.
+int build_tlas_node(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std::vector<HostBox> &boxes,
+                    std::vector<Bvh4Node> &nodes) {
+    if (e - b == 1) return make_leaf(ids[b], 1u);
+    uint32_t ranges[4][2];
+    int nk = 0;
+    const uint32_t m = sah_split(ids, b, e, boxes);
+    const uint32_t half[2][2] = {{b, m}, {m, e}};
+    for (auto &h : half) {
+        if (h[1] - h[0] > 1) {
+            const uint32_t mm = sah_split(ids, h[0], h[1], boxes);
+            ranges[nk][0] = h[0];
+            ranges[nk++][1] = mm;
+            ranges[nk][0] = mm;
+            ranges[nk++][1] = h[1];
+        } else {
+            ranges[nk][0] = h[0];
+            ranges[nk++][1] = h[1];
+        }
+    }
+    const uint32_t self = (uint32_t)nodes.size();
+    nodes.emplace_back();
+    int link[4];
+    float clo[3][4] = {}, chi[3][4] = {};
+    HostBox nb = HostBox::empty();
+    for (int k = 0; k < nk; k++) {
+        HostBox cb = HostBox::empty();
+        for (uint32_t i = ranges[k][0]; i < ranges[k][1]; i++) cb.grow(boxes[ids[i]]);
+        nb.grow(cb);
+        for (int a = 0; a < 3; a++) {
+            clo[a][k] = cb.lo[a];
+            chi[a][k] = cb.hi[a];
+        }
+        link[k] = build_tlas_node(ids, ranges[k][0], ranges[k][1], boxes, nodes);
+    }
+    nodes[self] = encode_bvh4(nb.lo, nb.hi, clo, chi, link, nk);
+    return (int)self;
+}
+
+// Object-space box margin of an instance (see accel_two_level.h).  A world hit
+// X = o + t d on the triangle fl(M v_k) maps through the float inverse A to
+// within c u |A| (|M| |v| + |m_t|) of the object triangle, and the computed
+// object ray fl(A o) + t fl(A d) differs from A X by c u (|A| (|o| + t |d|) + |a_t|),
+// c <= 8.  The margin uses 2^-18 = 32 u (a factor 4 of headroom) with infinity
+// norms, so an object-space BLAS box never culls a triangle the world-space
+// test reports.
+void instance_margin(DevInstance &d, float vmax) {
+    float anorm = 0.f, at = 0.f, mnorm = 0.f, mt = 0.f;
+    for (int r = 0; r < 3; r++) {
+        anorm = std::max(anorm, std::fabs(d.to_object[4 * r]) + std::fabs(d.to_object[4 * r + 1]) +
+                                    std::fabs(d.to_object[4 * r + 2]));
+        mnorm = std::max(mnorm, std::fabs(d.to_world[4 * r]) + std::fabs(d.to_world[4 * r + 1]) +
+                                    std::fabs(d.to_world[4 * r + 2]));
+        at = std::max(at, std::fabs(d.to_object[4 * r + 3]));
+        mt = std::max(mt, std::fabs(d.to_world[4 * r + 3]));
+    }
+    const float c = 0x1p-18f;
+    d.margin[0] = c * anorm;
+    d.margin[1] = c * (anorm * (mnorm * vmax + mt) + at);
+}
+
+}  // namespace
+
+int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstance *d_insts,
+                 const std::vector<uint32_t> &changed, hipStream_t s) {
+    const uint32_t n = (uint32_t)insts.size();
+    if (!changed.empty()) {
+        if (hipMemcpyAsync(acc.d_list, changed.data(), sizeof(uint32_t) * changed.size(), hipMemcpyHostToDevice, s) !=
+            hipSuccess)
+            return -1;
+        hipLaunchKernelGGL(k_inst_bounds, dim3((uint32_t)changed.size()), dim3(kBlock), 0, s, d_insts, acc.d_list,
+                           acc.d_verts, acc.d_boxes);
+        std::vector<float> h(6 * (size_t)n);
+        if (hipMemcpyAsync(h.data(), acc.d_boxes, sizeof(float) * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -1;
+        for (uint32_t id : changed) {
+            for (int k = 0; k < 3; k++) {
+                insts[id].wlo[k] = h[6 * (size_t)id + k];
+                insts[id].whi[k] = h[6 * (size_t)id + 3 + k];
+            }
+            if (hipMemcpyAsync(d_insts + id, &insts[id], sizeof(DevInstance), hipMemcpyHostToDevice, s) != hipSuccess)
+                return -1;
+        }
+    }
+    std::vector<HostBox> boxes(n);
+    for (uint32_t i = 0; i < n; i++)
+        for (int k = 0; k < 3; k++) {
+            boxes[i].lo[k] = insts[i].wlo[k];
+            boxes[i].hi[k] = insts[i].whi[k];
+        }
+    std::vector<uint32_t> ids;  // instances with geometry (an empty mesh has no BLAS)
+    for (uint32_t i = 0; i < n; i++)
+        if (insts[i].kind == PUPIL_SHAPE_SPHERE || insts[i].blas_root != kTraverseDone) ids.push_back(i);
+    std::vector<Bvh4Node> nodes;
+    const int root = ids.empty() ? kTraverseDone : build_tlas_node(ids, 0, (uint32_t)ids.size(), boxes, nodes);
+    if (nodes.size() > acc.tlas_cap) return -1;
+    if (!nodes.empty() &&
+        hipMemcpyAsync(acc.nodes4, nodes.data(), sizeof(Bvh4Node) * nodes.size(), hipMemcpyHostToDevice, s) !=
+            hipSuccess)
+        return -1;
+    acc.tlas_nodes = (uint32_t)nodes.size();
+    acc.root_link4 = (uint32_t)root;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
+}
+
+int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<uint32_t> &inst_shape,
+                    std::vector<DevInstance> &insts, DevInstance *d_insts, const DevMaterial *d_mats,
+                    uint32_t leaf_size, hipStream_t s, TwoLevelAccel &acc) {
+    const auto t0 = std::chrono::steady_clock::now();
+    acc = TwoLevelAccel{};
+    const uint32_t n = (uint32_t)insts.size();
+    // BLAS per mesh shape that some instance uses
+    std::vector<uint8_t> used(shapes.size(), 0);
+    std::vector<uint32_t> shape_of(n);
+    for (uint32_t i = 0; i < n; i++) {
+        shape_of[i] = insts[i].kind == PUPIL_SHAPE_SPHERE ? 0xFFFFFFFFu : inst_shape[i];
+        if (shape_of[i] != 0xFFFFFFFFu) used[shape_of[i]] = 1;
+    }
+    std::vector<BvhBuildOutput> blas(shapes.size());
+    std::vector<uint32_t> node_base(shapes.size(), 0), prim_base(shapes.size(), 0);
+    acc.tlas_cap = std::max(1u, n);
+    uint32_t total_nodes = acc.tlas_cap, total_prims = 0, max_faces = 1;
+    for (size_t k = 0; k < shapes.size(); k++)
+        if (used[k]) max_faces = std::max(max_faces, shapes[k].num_faces);
+    uint32_t *zeros = nullptr;
+    DevInstance *d_ident = nullptr;
+    int rc = 0;
+    if (hipMalloc((void **)&zeros, sizeof(uint32_t) * max_faces) != hipSuccess ||
+        hipMemset(zeros, 0, sizeof(uint32_t) * max_faces) != hipSuccess ||
+        hipMalloc((void **)&d_ident, sizeof(DevInstance)) != hipSuccess)
+        rc = -1;
+    for (size_t k = 0; k < shapes.size() && !rc; k++) {
+        if (!used[k]) continue;
+        const TwoLevelShape &sh = shapes[k];
+        DevInstance id{};
+        const float I[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        std::memcpy(id.to_world, I, sizeof(I));
+        std::memcpy(id.to_object, I, sizeof(I));
+        id.kind = PUPIL_SHAPE_MESH;
+        id.emitter_offset = -1;
+        id.positions = sh.positions;
+        id.normals = sh.normals;
+        id.texcoords = sh.texcoords;
+        id.indices = sh.indices;
+        if (hipMemcpy(d_ident, &id, sizeof(id), hipMemcpyHostToDevice) != hipSuccess) {
+            rc = -1;
+            break;
+        }
+        BvhBuildInput bin{sh.num_faces, zeros, d_ident, d_mats, 1u};
+        double ms = 0.0;
+        if (sh.num_faces && build_lbvh(bin, blas[k], leaf_size, s, &ms) != 0) {
+            rc = -1;
+            break;
+        }
+        node_base[k] = total_nodes;
+        prim_base[k] = total_prims;
+        total_nodes += blas[k].num_nodes4;
+        total_prims += sh.num_faces;
+    }
+    if (!rc && (hipMalloc((void **)&acc.nodes4, sizeof(Bvh4Node) * total_nodes) != hipSuccess ||
+                hipMalloc((void **)&acc.prims, sizeof(float4) * 3 * (size_t)std::max(1u, total_prims)) != hipSuccess ||
+                hipMalloc((void **)&acc.attrs, sizeof(float4) * kAttrStride * (size_t)std::max(1u, total_prims)) !=
+                    hipSuccess ||
+                hipMalloc((void **)&acc.d_boxes, sizeof(uint32_t) * 6 * (size_t)n) != hipSuccess ||
+                hipMalloc((void **)&acc.d_list, sizeof(uint32_t) * n) != hipSuccess ||
+                hipMalloc((void **)&acc.d_verts, sizeof(uint32_t) * n) != hipSuccess))
+        rc = -1;
+    for (size_t k = 0; k < shapes.size() && !rc; k++) {
+        if (!used[k]) continue;
+        const BvhBuildOutput &b = blas[k];
+        const uint32_t nf = shapes[k].num_faces;
+        if (nf == 0) continue;
+        if ((b.num_nodes4 && hipMemcpyAsync(acc.nodes4 + node_base[k], b.nodes4, sizeof(Bvh4Node) * b.num_nodes4,
+                                            hipMemcpyDeviceToDevice, s) != hipSuccess) ||
+            hipMemcpyAsync(acc.prims + 3 * (size_t)prim_base[k], b.prims, sizeof(float4) * 3 * (size_t)nf,
+                           hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(acc.attrs + kAttrStride * (size_t)prim_base[k], b.attrs, sizeof(float4) * kAttrStride * nf,
+                           hipMemcpyDeviceToDevice, s) != hipSuccess) {
+            rc = -1;
+            break;
+        }
+        if (b.num_nodes4)
+            hipLaunchKernelGGL(k_relink, dim3((b.num_nodes4 + kBlock - 1) / kBlock), dim3(kBlock), 0, s, acc.nodes4,
+                               b.num_nodes4, node_base[k], prim_base[k]);
+    }
+    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = -1;
+    for (auto &b : blas) free_lbvh(b);
+    if (zeros) (void)hipFree(zeros);
+    if (d_ident) (void)hipFree(d_ident);
+    if (rc) {
+        free_two_level(acc);
+        return rc;
+    }
+    acc.num_nodes4 = total_nodes;
+    acc.num_prims = total_prims;
+    // per instance: BLAS root / record base / margin, then the world boxes and the TLAS
+    std::vector<uint32_t> verts(n, 0), all(n);
+    for (uint32_t i = 0; i < n; i++) {
+        all[i] = i;
+        DevInstance &d = insts[i];
+        if (shape_of[i] == 0xFFFFFFFFu) {
+            d.blas_root = kTraverseDone;
+            d.attr_base = 0;
+            d.margin[0] = d.margin[1] = 0.f;
+            continue;
+        }
+        const uint32_t k = shape_of[i];
+        d.blas_root = shapes[k].num_faces ? rebase_link((int)blas[k].root_link4, node_base[k], prim_base[k])
+                                          : kTraverseDone;
+        d.attr_base = prim_base[k];
+        verts[i] = shapes[k].num_vertices;
+        instance_margin(d, shapes[k].vmax);
+    }
+    if (hipMemcpy(acc.d_verts, verts.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_insts, insts.data(), sizeof(DevInstance) * n, hipMemcpyHostToDevice) != hipSuccess ||
+        rebuild_tlas(acc, insts, d_insts, all, s) != 0) {
+        free_two_level(acc);
+        return -1;
+    }
+    acc.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+void free_two_level(TwoLevelAccel &acc) {
+    void *p[] = {acc.nodes4, acc.prims, acc.attrs, acc.d_boxes, acc.d_list, acc.d_verts};
+    for (void *x : p)
+        if (x) (void)hipFree(x);
+    acc = TwoLevelAccel{};
+}
+
+}  // namespace pupil

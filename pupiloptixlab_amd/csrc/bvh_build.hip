@@ -21,6 +21,7 @@
 #include <utility>
 #include <vector>
 
+#include "bvh4_quant.h"
 #include "pt_kernels.h"
 
 namespace pupil {
@@ -67,9 +68,15 @@ __global__ void k_prim_setup(BvhBuildInput in, float4 *recs, Aabb *boxes) {
         const uint32_t i0 = inst.indices[3 * local], i1 = inst.indices[3 * local + 1], i2 = inst.indices[3 * local + 2];
         const float *P = inst.positions;
         // world-space vertices: the CPU oracle applies the same row-major 3x4 product
-        const vec3 w0 = xform_point(inst.to_world, v3(P[3 * i0], P[3 * i0 + 1], P[3 * i0 + 2]));
-        const vec3 w1 = xform_point(inst.to_world, v3(P[3 * i1], P[3 * i1 + 1], P[3 * i1 + 2]));
-        const vec3 w2 = xform_point(inst.to_world, v3(P[3 * i2], P[3 * i2 + 1], P[3 * i2 + 2]));
+        // (object_space: a BLAS keeps the input vertices untouched)
+        vec3 w0 = v3(P[3 * i0], P[3 * i0 + 1], P[3 * i0 + 2]);
+        vec3 w1 = v3(P[3 * i1], P[3 * i1 + 1], P[3 * i1 + 2]);
+        vec3 w2 = v3(P[3 * i2], P[3 * i2 + 1], P[3 * i2 + 2]);
+        if (!in.object_space) {
+            w0 = xform_point(inst.to_world, w0);
+            w1 = xform_point(inst.to_world, w1);
+            w2 = xform_point(inst.to_world, w2);
+        }
         b.lo[0] = fminf(fminf(w0.x, w1.x), w2.x);
         b.lo[1] = fminf(fminf(w0.y, w1.y), w2.y);
         b.lo[2] = fminf(fminf(w0.z, w1.z), w2.z);
@@ -546,47 +553,6 @@ __global__ void k_flag4(int n, const int2 *ranges, const uint32_t *depth, uint32
     flags[i] = ((depth[i] & 1u) == 0u && (uint32_t)(r.y - r.x + 1) > leaf_size) ? 1u : 0u;
 }
 
-// decode used by the traversal: origin + (float)q * scale (q*scale is exact)
-__device__ __forceinline__ float qdecode(float origin, uint32_t q, float scale) { return origin + (float)q * scale; }
-
-// Conservative 8-bit quantisation of up to 4 child intervals on one axis.
-__device__ void quantize_axis(float lo, float hi, const float *clo, const float *chi, int nk, float &origin,
-                              uint32_t &ebyte, uint32_t &qlo, uint32_t &qhi) {
-    origin = lo;
-    const float ext = hi - lo;
-    float scale;
-    if (!(ext > 0.f)) {
-        scale = __uint_as_float(1u << 23);  // 2^-126
-    } else {
-        scale = exp2f(ceilf(log2f(ext / 254.f)));
-        if (!(scale > 0.f)) scale = __uint_as_float(1u << 23);
-    }
-    for (int attempt = 0; attempt < 8; attempt++) {
-        bool ok = true;
-        qlo = 0u;
-        qhi = 0u;
-        for (int k = 0; k < 4; k++) {
-            uint32_t a = 255u, b = 0u;  // empty slot: lo > hi
-            if (k < nk) {
-                float fa = floorf((clo[k] - origin) / scale);
-                float fb = ceilf((chi[k] - origin) / scale);
-                fa = fminf(fmaxf(fa, 0.f), 255.f);
-                fb = fminf(fmaxf(fb, 0.f), 255.f);
-                a = (uint32_t)fa;
-                b = (uint32_t)fb;
-                while (a > 0u && qdecode(origin, a, scale) > clo[k]) a--;
-                while (b < 255u && qdecode(origin, b, scale) < chi[k]) b++;
-                if (qdecode(origin, a, scale) > clo[k] || qdecode(origin, b, scale) < chi[k]) ok = false;
-            }
-            qlo |= a << (8 * k);
-            qhi |= b << (8 * k);
-        }
-        if (ok) break;
-        scale = scale * 2.f;
-    }
-    ebyte = (__float_as_uint(scale) >> 23) & 0xFFu;
-}
-
 __global__ void k_emit4(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
                         const int2 *ranges, const Aabb *node_boxes, const uint32_t *flags, const uint32_t *idx4,
                         uint32_t leaf_size, Bvh4Node *nodes4) {
@@ -749,7 +715,8 @@ __global__ void k_attrs(int n, const uint32_t *sorted_vals, BvhBuildInput in, fl
     const uint32_t prim = sorted_vals[i];
     const uint32_t inst_id = in.prim_inst[prim];
     const DevInstance &inst = in.instances[inst_id];
-    float4 *r = attrs + (size_t)kAttrStride * i;
+    // object_space (BLAS): records in the mesh's own primitive order, found by primitive id
+    float4 *r = attrs + (size_t)kAttrStride * (in.object_space ? prim : (uint32_t)i);
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     if (inst.kind == PUPIL_SHAPE_SPHERE) {
         r[0] = make_float4(0.f, 0.f, 0.f, __uint_as_float(prim | kPrimSphereBit));

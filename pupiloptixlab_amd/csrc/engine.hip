@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/pupil_pt.h"
+#include "accel_two_level.h"
 #include "pt_kernels.h"
 
 namespace {
@@ -87,6 +88,8 @@ struct pupil_pt {
     DeviceScene sc{};
     std::vector<void *> allocs;
     BvhBuildOutput bvh{};
+    bool two_level = false;  // TLAS + per-shape BLAS (accel_two_level.hip) instead of one flattened BVH
+    TwoLevelAccel tl{};
     uint32_t width = 0, height = 0, max_depth = 1;
     uint32_t num_prims = 0;
     uint32_t leaf_size = 3;  // primitives per BVH leaf (PUPIL_LEAF_SIZE)
@@ -155,6 +158,7 @@ struct pupil_pt {
         release_state();
         for (void *p : allocs) (void)hipFree(p);
         free_lbvh(bvh);
+        free_two_level(tl);
         if (pixel_map) (void)hipFree(pixel_map);
         for (auto e : trace_events) (void)hipEventDestroy(e);
         if (ev_begin) (void)hipEventDestroy(ev_begin);
@@ -441,6 +445,8 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         d.emitter_offset = src.emitter_offset;
         d.flip_normals = src.flip_normals;
         d.flip_tex_coords = src.flip_tex_coords;
+        d.bin = (mats[src.material].type >= 1u && mats[src.material].type <= 7u) ? mats[src.material].type : 8u;
+        d.blas_root = kTraverseDone;
         d.positions = shapes[src.shape].pos;
         d.normals = shapes[src.shape].nrm;
         d.texcoords = shapes[src.shape].tex;
@@ -451,7 +457,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         prim_inst.insert(prim_inst.end(), nprim, i);
     }
     pt->num_prims = (uint32_t)prim_inst.size();
-    if (pt->num_prims >= (1u << 28)) return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "more than 2^28 primitives"));
+    if (prim_inst.size() >= (1ull << 31)) return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "more than 2^31 primitives"));
     DevInstance *d_insts = nullptr;
     DevMaterial *d_mats = nullptr;
     uint32_t *d_prim_inst = nullptr;
@@ -462,32 +468,86 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         int rc = upload_emitters(pt, scene);
         if (rc) return cleanup(rc);
     }
-    pt->h_insts = insts;
     pt->d_insts = d_insts;
     pt->d_mats = d_mats;
     pt->d_prim_inst = d_prim_inst;
-    // LBVH (replaces GAS + IAS builds)
-    BvhBuildInput bin{pt->num_prims, d_prim_inst, d_insts, d_mats};
     pt->leaf_size = 3u;
     if (const char *ls = std::getenv("PUPIL_LEAF_SIZE")) pt->leaf_size = (uint32_t)std::min(8, std::max(1, std::atoi(ls)));
-    if (build_lbvh(bin, pt->bvh, pt->leaf_size, pt->own_stream, &pt->build_ms) != 0)
-        return cleanup(fail(PUPIL_ERR_HIP, "LBVH build failed"));
+    // Acceleration structure (replaces the GAS + IAS builds): one flattened BVH over
+    // world-space primitives (default: on config 5 it traces 3.2x faster than the
+    // two-level structure), or a TLAS over per-shape object-space BLASes
+    // (PUPIL_ACCEL=two_level; automatic when the flattened primitive count would pass
+    // the flat build's 2^28 limit).  Both give bit-identical hits.
+    {
+        std::vector<uint32_t> uses(scene->num_shapes, 0), inst_shape(scene->num_instances);
+        uint64_t flat_prims = 0;
+        for (uint32_t i = 0; i < scene->num_instances; i++) {
+            inst_shape[i] = scene->instances[i].shape;
+            uses[inst_shape[i]]++;
+            const pupil_shape &sh = scene->shapes[inst_shape[i]];
+            flat_prims += sh.kind == PUPIL_SHAPE_SPHERE ? 1u : sh.num_faces;
+        }
+        pt->two_level = flat_prims >= (1ull << 28);
+        if (const char *a = std::getenv("PUPIL_ACCEL")) {
+            if (std::strcmp(a, "flat") == 0) pt->two_level = false;
+            if (std::strcmp(a, "two_level") == 0) pt->two_level = true;
+        }
+        if (!pt->two_level && flat_prims >= (1ull << 28))
+            return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "flattened BVH limited to 2^28 primitives"));
+        if (pt->two_level) {
+            std::vector<TwoLevelShape> tls(scene->num_shapes);
+            for (uint32_t k = 0; k < scene->num_shapes; k++) {
+                const pupil_shape &sh = scene->shapes[k];
+                TwoLevelShape &t = tls[k];
+                t = TwoLevelShape{};
+                if (sh.kind != PUPIL_SHAPE_MESH || !uses[k]) continue;
+                t.num_faces = sh.num_faces;
+                t.num_vertices = sh.num_vertices;
+                t.positions = shapes[k].pos;
+                t.normals = shapes[k].nrm;
+                t.texcoords = shapes[k].tex;
+                t.indices = shapes[k].idx;
+                float vmax = 0.f;
+                for (size_t v = 0; v < 3 * (size_t)sh.num_vertices; v++) vmax = std::max(vmax, std::fabs(sh.positions[v]));
+                t.vmax = vmax;
+            }
+            if (build_two_level(tls, inst_shape, insts, d_insts, d_mats, pt->leaf_size, pt->own_stream, pt->tl) != 0)
+                return cleanup(fail(PUPIL_ERR_HIP, "two-level acceleration build failed"));
+            pt->build_ms = pt->tl.build_ms;
+        } else {
+            BvhBuildInput bin{pt->num_prims, d_prim_inst, d_insts, d_mats};
+            if (build_lbvh(bin, pt->bvh, pt->leaf_size, pt->own_stream, &pt->build_ms) != 0)
+                return cleanup(fail(PUPIL_ERR_HIP, "LBVH build failed"));
+        }
+    }
+    pt->h_insts = insts;
     DeviceScene &sc = pt->sc;
-    sc.nodes = pt->bvh.nodes;
-    sc.prims = pt->bvh.prims;
-    sc.attrs = pt->bvh.attrs;
     sc.num_prims = pt->num_prims;
-    sc.root_link = pt->bvh.root_link;
-    sc.nodes4 = pt->bvh.nodes4;
-    sc.root_link4 = pt->bvh.root_link4;
     sc.bvh_width = 4;
-    if (const char *w = std::getenv("PUPIL_BVH_WIDTH"))  // A/B switch for the node format
-        if (std::atoi(w) == 2) sc.bvh_width = 2;
+    if (pt->two_level) {
+        sc.two_level = 1;
+        sc.nodes = nullptr;
+        sc.root_link = (uint32_t)kTraverseDone;
+        sc.nodes4 = pt->tl.nodes4;
+        sc.prims = pt->tl.prims;
+        sc.attrs = pt->tl.attrs;
+        sc.root_link4 = pt->tl.root_link4;
+    } else {
+        sc.nodes = pt->bvh.nodes;
+        sc.prims = pt->bvh.prims;
+        sc.attrs = pt->bvh.attrs;
+        sc.root_link = pt->bvh.root_link;
+        sc.nodes4 = pt->bvh.nodes4;
+        sc.root_link4 = pt->bvh.root_link4;
+        if (const char *w = std::getenv("PUPIL_BVH_WIDTH"))  // A/B switch for the node format
+            if (std::atoi(w) == 2) sc.bvh_width = 2;
+    }
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pt->device);
     sc.num_cus = (uint32_t)std::max(1, cus);
     sc.trace_refill = 24;  // persistent BVH4 kernels; 0 selects the one-ray-per-lane kernels (A/B)
     if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
+    if (pt->two_level && sc.trace_refill == 0) sc.trace_refill = 24;  // two-level: persistent BVH4 kernels only
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
     sc.trace_node_min = 4;
@@ -507,7 +567,9 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         return cleanup(fail(PUPIL_ERR_HIP, "workspace clear failed"));
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
-    pt->totals.bvh_nodes = pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes;
+    pt->totals.bvh_nodes = pt->two_level ? pt->tl.tlas_nodes + (pt->tl.num_nodes4 - pt->tl.tlas_cap)
+                           : (pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes);
+    pt->totals.two_level = pt->two_level ? 1u : 0u;
     pt->totals.bvh_prims = pt->num_prims;
     pt->totals.build_ms = pt->build_ms;
     *out = pt;
@@ -534,6 +596,15 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     std::memcpy(d.to_world, to_world, sizeof(d.to_world));
     std::memcpy(d.to_object, to_object, sizeof(d.to_object));
     HIP_TRY(hipMemcpy(pt->d_insts + instance, &d, sizeof(DevInstance), hipMemcpyHostToDevice));
+    if (pt->two_level) {  // new world box for the instance, TLAS rebuilt over all instance boxes
+        const auto t0 = std::chrono::steady_clock::now();
+        if (rebuild_tlas(pt->tl, pt->h_insts, pt->d_insts, {instance}, pt->own_stream) != 0)
+            return fail(PUPIL_ERR_HIP, "TLAS rebuild failed");
+        pt->sc.root_link4 = pt->tl.root_link4;
+        pt->totals.bvh_nodes = pt->tl.tlas_nodes + (pt->tl.num_nodes4 - pt->tl.tlas_cap);
+        pt->totals.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return PUPIL_OK;
+    }
     BvhBuildInput bin{pt->num_prims, pt->d_prim_inst, pt->d_insts, pt->d_mats};
     BvhBuildOutput nb{};
     double ms = 0.0;

@@ -10,6 +10,7 @@ namespace pupil {
 
 constexpr int kTraceBlock = 128;
 constexpr int kTraceWavesPerSimd = 6;  // persistent BVH4 kernels: occupancy target (<= 80 VGPRs)
+constexpr int kTraceWavesPerSimdTL = 4;  // two-level variant (<= 128 VGPRs)
 constexpr int kStackLds = 32;   // per-thread LDS stack entries
 constexpr int kStackOvf = 96;   // per-thread global overflow entries
 constexpr int kShadeBlock = 256;
@@ -123,6 +124,7 @@ struct BvhBuildInput {
     const uint32_t *prim_inst;      // device, global prim -> instance
     const DevInstance *instances;   // device
     const DevMaterial *materials;   // device
+    uint32_t object_space;          // 1: BLAS build (vertices untransformed, shading records in primitive order)
 };
 struct BvhBuildOutput {
     BvhNode *nodes;     // device, max(1, n-1)

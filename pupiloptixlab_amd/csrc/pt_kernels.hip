@@ -189,6 +189,45 @@ __device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const 
     return false;
 }
 
+// Two-level BLAS leaf: object-space triangle records of instance `inst`,
+// tested in world space on fl(to_world * v) (the flattened build's and the
+// oracle's world vertices), keyed by the global primitive id.
+template <bool STATS>
+__device__ __forceinline__ bool intersect_leaf_tl(const DeviceScene &sc, const RayPre &r, int leaf, uint32_t inst,
+                                                  float tmin, float &tmax, uint32_t &best_key, uint32_t &best_idx,
+                                                  float &bb1, float &bb2, uint32_t &prims_tested, bool &found,
+                                                  bool any) {
+    const DevInstance &in = sc.instances[inst];
+    const uint32_t first = leaf_first(leaf);
+    const uint32_t count = leaf_count(leaf);
+    for (uint32_t i = first; i < first + count; i++) {
+        const float4 a = sc.prims[3 * i + 0];
+        const float4 b = sc.prims[3 * i + 1];
+        const float4 c = sc.prims[3 * i + 2];
+        const uint32_t key = in.prim_offset + __float_as_uint(a.w);
+        if (STATS) prims_tested++;
+        float t, b1 = 0.f, b2 = 0.f;
+        const vec3 w0 = xform_point(in.to_world, v3(a.x, a.y, a.z));
+        const vec3 w1 = xform_point(in.to_world, v3(b.x, b.y, b.z));
+        const vec3 w2 = xform_point(in.to_world, v3(c.x, c.y, c.z));
+        if (intersect_triangle(r, w0, w1, w2, tmin, tmax, t, b1, b2)) {
+            if (any) {
+                found = true;
+                return true;
+            }
+            if (t < tmax || key < best_key) {
+                tmax = t;
+                best_key = key;
+                best_idx = key;
+                bb1 = b1;
+                bb2 = b2;
+                found = true;
+            }
+        }
+    }
+    return false;
+}
+
 template <bool ANY, bool STATS>
 __device__ __forceinline__ bool intersect_leaf(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
                                                float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
@@ -485,30 +524,35 @@ struct AxisTerms {
     float an, af;  // (o_node - o_ray) * idir - E, + E
 };
 
-__device__ __forceinline__ AxisTerms axis_terms(float onode, float s, float oray, float idir) {
+// PAD (two-level BLAS nodes): the object-space ray carries a position margin
+// `pad` (DevInstance::margin), added to the bound before scaling by |idir|.
+template <bool PAD>
+__device__ __forceinline__ AxisTerms axis_terms(float onode, float s, float oray, float idir, float pad) {
     AxisTerms t;
     const float A = onode - oray;
     const float a = A * idir;
-    const float e = __builtin_fmaf(512.f, s, fabsf(A) + fabsf(onode)) * (fabsf(idir) * 0x1p-21f);
+    const float e = PAD ? __builtin_fmaf(__builtin_fmaf(512.f, s, fabsf(A) + fabsf(onode)), 0x1p-21f, pad) * fabsf(idir)
+                        : __builtin_fmaf(512.f, s, fabsf(A) + fabsf(onode)) * (fabsf(idir) * 0x1p-21f);
     t.b = s * idir;
     t.an = a - e;
     t.af = a + e;
     return t;
 }
 
-__device__ __forceinline__ void visit4(const Bvh4Node &n, const RayPre &r, float tmin, float tmax, float t[4],
-                                       int l[4]) {
+template <bool PAD>
+__device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, float pad, float tmin, float tmax,
+                                       float t[4], int l[4]) {
     constexpr float kInf = __builtin_huge_valf();
     const float sx = __uint_as_float((n.exps & 0xFFu) << 23);
     const float sy = __uint_as_float(((n.exps >> 8) & 0xFFu) << 23);
     const float sz = __uint_as_float(((n.exps >> 16) & 0xFFu) << 23);
-    const bool px = r.idir.x >= 0.f, py = r.idir.y >= 0.f, pz = r.idir.z >= 0.f;
+    const bool px = ridir.x >= 0.f, py = ridir.y >= 0.f, pz = ridir.z >= 0.f;
     const uint32_t nx = px ? n.qlo_x : n.qhi_x, fx = px ? n.qhi_x : n.qlo_x;
     const uint32_t ny = py ? n.qlo_y : n.qhi_y, fy = py ? n.qhi_y : n.qlo_y;
     const uint32_t nz = pz ? n.qlo_z : n.qhi_z, fz = pz ? n.qhi_z : n.qlo_z;
-    const AxisTerms X = axis_terms(n.ox, sx, r.o.x, r.idir.x);
-    const AxisTerms Y = axis_terms(n.oy, sy, r.o.y, r.idir.y);
-    const AxisTerms Z = axis_terms(n.oz, sz, r.o.z, r.idir.z);
+    const AxisTerms X = axis_terms<PAD>(n.ox, sx, ro.x, ridir.x, pad);
+    const AxisTerms Y = axis_terms<PAD>(n.oy, sy, ro.y, ridir.y, pad);
+    const AxisTerms Z = axis_terms<PAD>(n.oz, sz, ro.z, ridir.z, pad);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const float tn = fmaxf(fmaxf(fmaxf(__builtin_fmaf(ubyte(nx, k), X.b, X.an), __builtin_fmaf(ubyte(ny, k), Y.b, Y.an)),
@@ -527,11 +571,34 @@ __device__ __forceinline__ void visit4(const Bvh4Node &n, const RayPre &r, float
     csel(t[1], l[1], t[2], l[2]);
 }
 
-template <int MODE, bool ANY, bool STATS>
-__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4(DeviceScene sc, PathState ps, Queues q, TraceJob job,
-                                                        int *ovf, uint32_t ovf_threads, TraceStats stats) {
+// Two-level: the object-space box ray of instance `in` (origin, reciprocal
+// direction) and its position margin at the exit of the instance's world box.
+__device__ __forceinline__ void enter_instance(const DevInstance &in, const RayPre &r, float tmax, vec3 &bo, vec3 &bi,
+                                               float &pad) {
+    bo = xform_point(in.to_object, r.o);
+    const vec3 d = xform_vector(in.to_object, r.d);
+    const float tiny = 1e-30f;
+    bi = v3(1.f / (fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x), 1.f / (fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y),
+            1.f / (fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z));
+    float te = tmax;
+    te = fminf(te, fmaxf((in.wlo[0] - r.o.x) * r.idir.x, (in.whi[0] - r.o.x) * r.idir.x));
+    te = fminf(te, fmaxf((in.wlo[1] - r.o.y) * r.idir.y, (in.whi[1] - r.o.y) * r.idir.y));
+    te = fminf(te, fmaxf((in.wlo[2] - r.o.z) * r.idir.z, (in.whi[2] - r.o.z) * r.idir.z));
+    te = fabsf(te) * 1.0001f;
+    const float on = fmaxf(fmaxf(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z));
+    const float dn = fmaxf(fmaxf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
+    pad = __builtin_fmaf(in.margin[0], __builtin_fmaf(te, dn, on), in.margin[1]);
+}
+
+// TL = two-level acceleration (DeviceScene::two_level): the TLAS leaves hold one
+// instance each; entering one pushes the pending TLAS link and kReturnLink and
+// switches the box tests to the instance's object-space ray; popping
+// kReturnLink switches back.  Spheres are tested at their TLAS leaf.
+template <int MODE, bool ANY, bool STATS, bool TL>
+__device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathState &ps, const Queues &q,
+                                            const TraceJob &job, int *ovf, uint32_t ovf_threads,
+                                            const TraceStats &stats, int *s_ring) {
     constexpr float kInf = __builtin_huge_valf();
-    __shared__ int s_ring[kRing * kTraceBlock];
     const uint32_t n_next = MODE == kModeMixed ? q.counts[kCntNext] : 0u;
     const uint32_t count =
         MODE == kModeShadow ? q.counts[kCntShadow]
@@ -562,6 +629,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     int node = kSentinel, leaf = 0;
     bool found = false;
     bool any = ANY;  // this lane's ray terminates on its first hit
+    bool in_blas = false;  // TL: traversing an instance's BLAS
+    uint32_t inst = 0;
+    vec3 bo = v3(0.f), bi = v3(0.f);  // TL: box-test ray (object space inside a BLAS)
+    float bpad = 0.f;
     for (;;) {
         // ---- refill idle lanes (one atomic per wave)
         const unsigned long long idle = __ballot(!active);
@@ -620,6 +691,12 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                     st.reset();
                     node = (int)sc.root_link4;
                     leaf = 0;
+                    if (TL) {
+                        in_blas = false;
+                        bo = r.o;
+                        bi = r.idir;
+                        bpad = 0.f;
+                    }
                     if (node < 0) {
                         leaf = node;
                         node = kSentinel;
@@ -647,7 +724,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                 }
                 float t[4];
                 int l[4];
-                visit4(n, r, tmin, tmax, t, l);
+                if (TL) visit4<true>(n, bo, bi, bpad, tmin, tmax, t, l);
+                else visit4<false>(n, r.o, r.idir, 0.f, tmin, tmax, t, l);
                 if (t[0] == kInf) {
                     node = st.pop();
                 } else {
@@ -672,11 +750,61 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
                         dg[3] += (unsigned long long)__popcll(m);
                     }
                 }
-                if (intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2,
-                                              MODE == kModeMixed && any ? npt_sh : npt, found, any))
+                uint32_t &np_cnt = MODE == kModeMixed && any ? npt_sh : npt;
+                if (TL && !in_blas) {  // a TLAS leaf: one instance
+                    const uint32_t id = leaf_first(leaf);
+                    const DevInstance &in = sc.instances[id];
+                    if (in.kind == PUPIL_SHAPE_SPHERE) {
+                        if (STATS) np_cnt++;
+                        float ts;
+                        if (intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, ts)) {
+                            if (any) {
+                                found = true;
+                                break;
+                            }
+                            if (ts < tmax || in.prim_offset < best_key) {
+                                tmax = ts;
+                                best_key = best_idx = in.prim_offset;
+                                b1 = b2 = 0.f;
+                                found = true;
+                            }
+                        }
+                    } else {  // enter its BLAS; the pending TLAS link resumes after kReturnLink
+                        st.reserve3();
+                        st.push(node, true);
+                        st.push(kReturnLink, true);
+                        in_blas = true;
+                        inst = id;
+                        enter_instance(in, r, tmax, bo, bi, bpad);
+                        node = in.blas_root;
+                        leaf = 0;
+                        if (node < 0) {
+                            leaf = node;
+                            node = st.pop();
+                        }
+                        continue;
+                    }
+                } else if (TL) {
+                    if (intersect_leaf_tl<STATS>(sc, r, leaf, inst, tmin, tmax, best_key, best_idx, b1, b2, np_cnt,
+                                                 found, any))
+                        break;
+                } else if (intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, np_cnt,
+                                                     found, any)) {
                     break;
+                }
                 leaf = node;
                 if (node < 0) node = st.pop();
+            }
+            if (TL && node == kReturnLink && leaf >= 0 && !(any && found)) {  // BLAS exhausted: back to the TLAS
+                in_blas = false;
+                bo = r.o;
+                bi = r.idir;
+                bpad = 0.f;
+                node = st.pop();
+                if (node < 0) {
+                    leaf = node;
+                    node = st.pop();
+                }
             }
         }
         const bool done = active && ((node == kSentinel && leaf >= 0) || (any && found));
@@ -686,8 +814,12 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
             if (done && !any) {
                 ps.hit[p] = make_float4(found ? tmax : -1.f, b1, b2, __uint_as_float(found ? best_idx : kMissIndex));
                 if (found) {
-                    const uint32_t mt = __float_as_uint(sc.prims[3 * best_idx + 2].w);
-                    bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
+                    if (TL) {
+                        bin = sc.instances[sc.prim_inst[best_idx]].bin;
+                    } else {
+                        const uint32_t mt = __float_as_uint(sc.prims[3 * best_idx + 2].w);
+                        bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
+                    }
                 }
                 ps.mbin[p] = (uint8_t)bin;  // material bin for the partition
             }
@@ -727,6 +859,22 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
         if (lane_id() == 0)
             for (int k = 0; k < 6; k++) atomicAdd(&stats.counters[(MODE == kModeShadow ? 8 : 2) + k], dg[k]);
     }
+}
+
+template <int MODE, bool ANY, bool STATS>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4(
+    DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
+    __shared__ int s_ring[kRing * kTraceBlock];
+    trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring);
+}
+
+// two-level variant: 9 more live registers (object-space box ray, margin,
+// instance) -> one wave less per SIMD so the loop does not spill
+template <int MODE, bool ANY, bool STATS>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimdTL))) void k_trace4tl(
+    DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
+    __shared__ int s_ring[kRing * kTraceBlock];
+    trace4_body<MODE, ANY, STATS, true>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring);
 }
 
 // ------------------------------------------------------------------ generate
@@ -776,18 +924,30 @@ struct HitGeo {
 __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, vec3 ro, vec3 rd, vec2 stale_uv) {
     HitGeo out;
     const uint32_t idx = __float_as_uint(h.w);
-    const float4 *rec = sc.attrs + (size_t)kAttrStride * idx;
-    const float4 a = rec[0];
-    const float4 b = rec[1];
-    const uint32_t ref = __float_as_uint(a.w);
-    const uint32_t gprim = ref & ~kPrimSphereBit;
-    const uint32_t inst_id = __float_as_uint(b.w);
+    // flat: idx = record in traversal order, which names the instance; two-level:
+    // idx = global primitive id -> instance -> the shape's record in primitive order
+    uint32_t inst_id, gprim;
+    bool sphere;
+    const float4 *rec;
+    if (sc.two_level) {
+        gprim = idx;
+        inst_id = sc.prim_inst[idx];
+        const DevInstance &ti = sc.instances[inst_id];
+        sphere = ti.kind == PUPIL_SHAPE_SPHERE;
+        rec = sc.attrs + (size_t)kAttrStride * (sphere ? 0u : ti.attr_base + (idx - ti.prim_offset));
+    } else {
+        rec = sc.attrs + (size_t)kAttrStride * idx;
+        const uint32_t ref = __float_as_uint(rec[0].w);
+        gprim = ref & ~kPrimSphereBit;
+        sphere = (ref & kPrimSphereBit) != 0u;
+        inst_id = __float_as_uint(rec[1].w);
+    }
     const DevInstance &in = sc.instances[inst_id];
     out.inst = inst_id;
     LocalGeo &g = out.g;
     g.texcoord = stale_uv;
     uint32_t local = 0;
-    if (ref & kPrimSphereBit) {
+    if (sphere) {
         g.position = ro + h.x * rd;
         const vec3 local_pos = xform_point(in.to_object, g.position);
         g.texcoord = sphere_texcoord(normalize(local_pos - v3(0.f)));
@@ -795,6 +955,8 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, v
         if (in.flip_normals) g.normal = g.normal * -1.f;
     } else {
         local = gprim - in.prim_offset;
+        const float4 a = rec[0];
+        const float4 b = rec[1];
         const float4 c = rec[2];
         const vec3 p0 = v3(a.x, a.y, a.z);
         const vec3 p1 = v3(b.x, b.y, b.z);
@@ -1111,8 +1273,31 @@ __global__ void k_debug_math(const float *x, const float *y2, float *out, uint32
 
 // Persistent grid: exactly the resident capacity (CUs x 4 SIMDs x waves per SIMD).
 static uint32_t trace4_blocks(const DeviceScene &sc, uint32_t ovf_threads) {
-    const uint32_t resident = sc.num_cus * 4u * (uint32_t)kTraceWavesPerSimd / (kTraceBlock / 64u);
+    const uint32_t waves = sc.two_level ? kTraceWavesPerSimdTL : kTraceWavesPerSimd;
+    const uint32_t resident = sc.num_cus * 4u * waves / (kTraceBlock / 64u);
     return std::min(ovf_threads / kTraceBlock, std::max(1u, resident));
+}
+
+// persistent BVH4 traversal launch: flat or two-level variant, with or without counters
+template <int MODE, bool ANY>
+static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queues &q, const TraceJob &job, int *ovf,
+                          uint32_t ovf_threads, const TraceStats *stats, hipStream_t s) {
+    const TraceStats st = stats ? *stats : TraceStats{nullptr};
+    const uint32_t blocks = trace4_blocks(sc, ovf_threads);
+    if (sc.two_level) {
+        if (stats)
+            hipLaunchKernelGGL((k_trace4tl<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                               ovf, ovf_threads, st);
+        else
+            hipLaunchKernelGGL((k_trace4tl<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                               ovf, ovf_threads, st);
+    } else if (stats) {
+        hipLaunchKernelGGL((k_trace4<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
+                           ovf_threads, st);
+    } else {
+        hipLaunchKernelGGL((k_trace4<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
+                           ovf_threads, st);
+    }
 }
 
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
@@ -1120,7 +1305,14 @@ void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, ui
     if (sc.bvh_width == 4 && sc.trace_refill) {  // the production kernel, fed from a ray array
         const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, sc.trace_node_min, rays, out};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
-        if (any)
+        if (sc.two_level) {
+            if (any)
+                hipLaunchKernelGGL((k_trace4tl<kModeRays, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
+                                   PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
+            else
+                hipLaunchKernelGGL((k_trace4tl<kModeRays, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
+                                   PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
+        } else if (any)
             hipLaunchKernelGGL((k_trace4<kModeRays, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
                                PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
         else
@@ -1152,13 +1344,7 @@ void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     const bool w4 = sc.bvh_width == 4;
     if (w4 && sc.trace_refill) {
         const TraceJob job{queue, queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
-        const uint32_t blocks = trace4_blocks(sc, ovf_threads);
-        if (stats)
-            hipLaunchKernelGGL((k_trace4<kModeExtend, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
-                               job, ovf, ovf_threads, st);
-        else
-            hipLaunchKernelGGL((k_trace4<kModeExtend, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps,
-                               q, job, ovf, ovf_threads, st);
+        launch_trace4<kModeExtend, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
         return;
     }
 #define EXTEND(S, W)                                                                                      \
@@ -1181,13 +1367,7 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     const bool w4 = sc.bvh_width == 4;
     if (w4 && sc.trace_refill) {
         const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkShadow, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
-        const uint32_t blocks = trace4_blocks(sc, ovf_threads);
-        if (stats)
-            hipLaunchKernelGGL((k_trace4<kModeShadow, true, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
-                               job, ovf, ovf_threads, st);
-        else
-            hipLaunchKernelGGL((k_trace4<kModeShadow, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q,
-                               job, ovf, ovf_threads, st);
+        launch_trace4<kModeShadow, true>(sc, ps, q, job, ovf, ovf_threads, stats, s);
         return;
     }
 #define SHADOW(S, W)\
@@ -1204,15 +1384,8 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
 
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                         const TraceStats *stats, hipStream_t s) {
-    TraceStats st = stats ? *stats : TraceStats{nullptr};
     const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
-    const uint32_t blocks = trace4_blocks(sc, ovf_threads);
-    if (stats)
-        hipLaunchKernelGGL((k_trace4<kModeMixed, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
-                           ovf, ovf_threads, st);
-    else
-        hipLaunchKernelGGL((k_trace4<kModeMixed, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
-                           ovf, ovf_threads, st);
+    launch_trace4<kModeMixed, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
 }
 
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,

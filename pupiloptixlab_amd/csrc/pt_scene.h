@@ -78,6 +78,12 @@ struct DevInstance {
     const float *normals;
     const float *texcoords;
     const uint32_t *indices;
+    // two-level acceleration (DeviceScene::two_level; see accel_two_level.hip)
+    int32_t blas_root;    // link of the shape's BLAS root in the combined BVH4 node array
+    uint32_t attr_base;   // first shading record of the shape's BLAS primitives (local order)
+    uint32_t bin;         // material bin of the instance's hits (0 miss, 1..7 EMatType, 8 unknown)
+    float margin[2];      // object-space box margin: margin[0] * (|o| + t |d|) + margin[1]
+    float wlo[3], whi[3];  // world box of the instance's world-space primitives
 };
 
 struct alignas(16) BvhNode {
@@ -103,6 +109,9 @@ constexpr int kEmptyLink = 0x7FFFFFFF;
 // Traversal terminator (stack bottom); also the root link of an empty scene.
 // Inner-node links are < kTraverseDone, leaf links are negative.
 constexpr int kTraverseDone = 0x76543210;
+// Two-level traversal: stack marker below a BLAS's entries; popping it returns
+// the lane to the TLAS (a positive link above kTraverseDone, never a node index).
+constexpr int kReturnLink = 0x7654321F;
 
 // Child link encoding: link >= 0 -> internal node index; link < 0 -> leaf,
 // ~link = (first_prim << 3) | (count - 1), count in [1, 8].
@@ -131,6 +140,8 @@ struct DeviceScene {
     uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
     uint32_t num_cus;       // compute units of the device (persistent grid size)
     uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node
+    uint32_t two_level;       // 1: nodes4 = TLAS over instances + object-space BLAS per shape;
+                              //    prims/attrs = BLAS records, hit index = global primitive id
     const uint32_t *prim_inst;  // global prim id -> instance
     const DevInstance *instances;
     const DevMaterial *materials;

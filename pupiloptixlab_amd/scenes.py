@@ -242,10 +242,11 @@ def blas_mesh(num_spheres=125, seed=2, box=4.0, slices=40, stacks=26):
 
 
 def instanced_field(num_instances=40, width=3840, height=2160, max_depth=6, seed=2, spheres_per_blas=125,
-                    slices=40, stacks=26) -> W.World:
+                    slices=40, stacks=26, scale_range=None) -> W.World:
     """Config 5: ``num_instances`` instances of one 250k-triangle BLAS under random
     rigid transforms (seed 2), alternating rough dielectric (alpha 0.35) and rough
-    plastic (alpha 0.35), material_test.xml parameters, inside the config-4 room."""
+    plastic (alpha 0.35), material_test.xml parameters, inside the config-4 room.
+    scale_range=(lo, hi) adds a random non-uniform scale per instance (tests)."""
     wd = W.World()
     wd.set_film(width, height, max_depth)
     pos, idx, nrm, uv = blas_mesh(spheres_per_blas, seed, 4.0, slices, stacks)
@@ -259,8 +260,11 @@ def instanced_field(num_instances=40, width=3840, height=2160, max_depth=6, seed
         axis /= np.linalg.norm(axis)
         angle = float(rng.uniform(0.0, 360.0))
         t = (float(rng.uniform(-5.0, 5.0)), float(rng.uniform(2.5, 11.5)), float(rng.uniform(-7.0, 8.0)))
+        scale = (1.0, 1.0, 1.0)
+        if scale_range is not None:
+            scale = tuple(float(x) for x in rng.uniform(scale_range[0], scale_range[1], 3))
         wd.add_instance(blas, m_diel if k % 2 == 0 else m_plas,
-                        W.transform(rotate=(tuple(axis), angle), translate=t))
+                        W.transform(scale=scale, rotate=(tuple(axis), angle), translate=t))
     _room_and_light(wd)
     return wd
 

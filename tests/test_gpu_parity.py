@@ -127,13 +127,17 @@ def test_cornell_parity_config1():
         (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
 
 
-def test_materials_parity_config2():
-    """Config 2 (all seven BSDFs, spheres + boxes) at 192^2, 8 spp, depth 6."""
+@pytest.mark.parametrize("accel", ["flat", "two_level"])
+def test_materials_parity_config2(accel, monkeypatch):
+    """Config 2 (all seven BSDFs, spheres + boxes) at 192^2, 8 spp, depth 6; one flattened
+    BVH, or a TLAS over the mesh and sphere instances."""
+    monkeypatch.setenv("PUPIL_ACCEL", accel)
     p = scenes.cornell_materials_xml(os.path.join(TMP, "cbmat.xml"), 192, 192, 6)
     desc = World().load_scene(p).desc()
     gpu = render_gpu(desc, 8)
+    assert gpu["stats"]["two_level"] == (accel == "two_level")
     ref = oracle.OracleScene(desc).render(spp=8)
-    compare(gpu, ref, "materials192x8")
+    assert compare(gpu, ref, f"materials192x8-{accel}") == 192 * 192
 
 
 @pytest.mark.parametrize("width", ["2", "4"])
@@ -209,6 +213,30 @@ def test_field_hits_random_rays_all_traversals(monkeypatch):
         assert np.array_equal(occ[:, 0] > 0, ref[:, 0] > 0), f"bvh{width} refill {refill}: any-hit differs"
 
 
+@pytest.mark.parametrize("accel", ["flat", "two_level"])
+def test_instanced_hits_random_rays(accel, monkeypatch):
+    """Closest and any hits of 100k random rays among 12 instances of one BLAS under rotations,
+    non-uniform scales and translations: the two-level traversal (object-space BLAS boxes,
+    world-space triangle tests) equals the flattened BVH and the oracle bit for bit."""
+    monkeypatch.setenv("PUPIL_ACCEL", accel)
+    w = scenes.instanced_field(num_instances=12, width=32, height=18, max_depth=4, seed=3, spheres_per_blas=10,
+                               scale_range=(0.4, 2.5))
+    desc = w.desc()
+    rng = np.random.default_rng(13)
+    n = 100000
+    org = rng.uniform([-12, 0.1, -12], [12, 14, 12], (n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([org, d], 1).astype(np.float32)
+    ref = oracle.OracleScene(desc).closest(rays)
+    assert (ref[:, 0] > 0).mean() > 0.3
+    out = _trace(desc, rays)
+    bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
+    assert not bad.any(), f"{accel}: {bad.sum()} rays differ"
+    occ = _trace(desc, rays, any_hit=1)
+    assert np.array_equal(occ[:, 0] > 0, ref[:, 0] > 0)
+
+
 def _quad_stack(n, spacing=0.01):
     """n parallel unit quads stacked along z: every ray along z crosses all of them, so the
     traversal stack grows past the 16-entry LDS ring and spills to HBM."""
@@ -227,7 +255,9 @@ def _quad_stack(n, spacing=0.01):
     return w
 
 
-def test_deep_stack_spills_match_oracle(monkeypatch):
+@pytest.mark.parametrize("accel", ["flat", "two_level"])
+def test_deep_stack_spills_match_oracle(accel, monkeypatch):
+    monkeypatch.setenv("PUPIL_ACCEL", accel)
     w = _quad_stack(6000)
     desc = w.desc()
     rng = np.random.default_rng(5)
@@ -241,17 +271,19 @@ def test_deep_stack_spills_match_oracle(monkeypatch):
     rays = np.concatenate([org, d], 1).astype(np.float32)
     ref = oracle.OracleScene(desc).closest(rays)
     assert (ref[:, 0] > 0).mean() > 0.9
-    for width, refill in TRAVERSALS:
+    for width, refill in TRAVERSALS if accel == "flat" else [("4", "24")]:
         monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
         monkeypatch.setenv("PUPIL_REFILL", refill)
         out = _trace(desc, rays)
         bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
-        assert not bad.any(), f"bvh{width} refill {refill}: {bad.sum()} rays differ"
+        assert not bad.any(), f"{accel} bvh{width} refill {refill}: {bad.sum()} rays differ"
 
 
+@pytest.mark.parametrize("accel", ["flat", "two_level"])
 @pytest.mark.parametrize("ntri", [1, 2, 4, 5])
-def test_tiny_scenes(ntri, monkeypatch):
+def test_tiny_scenes(ntri, accel, monkeypatch):
     """The root is a leaf (<= 4 primitives): traversal terminates and hits match."""
+    monkeypatch.setenv("PUPIL_ACCEL", accel)
     w = World()
     tri_pos = np.array([[-1, -1, 0], [1, -1, 0], [0, 1, 0]], np.float32)
     pos = np.concatenate([tri_pos + [0, 0, 0.1 * k] for k in range(ntri)]).astype(np.float32)
@@ -266,7 +298,7 @@ def test_tiny_scenes(ntri, monkeypatch):
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.concatenate([org, d], 1).astype(np.float32)
     ref = oracle.OracleScene(desc).closest(rays)
-    for width, refill in TRAVERSALS:
+    for width, refill in TRAVERSALS if accel == "flat" else [("4", "24")]:
         monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
         monkeypatch.setenv("PUPIL_REFILL", refill)
         out = _trace(desc, rays)
@@ -313,26 +345,31 @@ def test_non_accumulating_frame_overwrites():
     assert np.array_equal(a["pt accum buffer"], b["pt accum buffer"])
 
 
-def test_instanced_rough_materials_parity():
+@pytest.mark.parametrize("accel", ["flat", "two_level"])
+def test_instanced_rough_materials_parity(accel, monkeypatch):
     """Config 5 in miniature: instances of one BLAS under rigid transforms, rough dielectric +
-    rough plastic, depth 6 (scenes.instanced_field)."""
+    rough plastic, depth 6 (scenes.instanced_field); flattened or two-level acceleration."""
+    monkeypatch.setenv("PUPIL_ACCEL", accel)
     w = scenes.instanced_field(num_instances=6, width=160, height=90, max_depth=6, seed=2, spheres_per_blas=12)
     desc = w.desc()
     gpu = render_gpu(desc, 4)
     ref = oracle.OracleScene(desc).render(spp=4)
-    exact = compare(gpu, ref, "instanced6x12")
+    exact = compare(gpu, ref, f"instanced6x12-{accel}")
+    assert gpu["stats"]["two_level"] == (accel == "two_level")
     s, rs = gpu["stats"], ref["stats"]
     assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
         (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
     assert exact == 160 * 90
 
 
-def test_instance_update_equals_fresh_engine():
+@pytest.mark.parametrize("accel", ["flat", "two_level"])
+def test_instance_update_equals_fresh_engine(accel, monkeypatch):
     """RenderInstanceUpdate: moving a sphere instance and the emissive light through
     World.set_instance_transform + PTPass.update_instance renders exactly what a
     freshly created engine (and the oracle) renders for the moved scene."""
     from pupiloptixlab_amd.pt_pass import PTPass
 
+    monkeypatch.setenv("PUPIL_ACCEL", accel)
     w = scenes.sphere_field(8, 96, 64, 4, seed=5, merge=False)
     desc0 = w.desc()
     n = desc0.num_instances
