@@ -50,11 +50,16 @@ def main():
             torch.cuda.synchronize()
             per_rank.append((time.perf_counter() - t0) / args.frames * 1e3)
             host_ms.append(host / args.frames * 1e3)
+            if r == 0:
+                st = pt.stats()
+                stage0 = {"trace_ms": round(st["trace_ms"], 3), "trace_launches": st["trace_launches"],
+                          "shade_ms": round(st["shade_ms"], 3),
+                          "rays": st["primary_rays"] + st["extension_rays"] + st["shadow_rays"]}
         worst = max(per_rank)
         base = base or worst * 1.0
         print(json.dumps({"world": n, "ms_max": round(worst, 3), "ms_min": round(min(per_rank), 3),
                           "pred_speedup": round(base / worst, 3), "pred_eff": round(base / worst / n, 3),
-                          "host_enqueue_ms": round(max(host_ms), 3),
+                          "host_enqueue_ms": round(max(host_ms), 3), "rank0": stage0,
                           "ms_per_rank": [round(x, 3) for x in per_rank]}), flush=True)
 
 
