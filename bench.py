@@ -109,8 +109,8 @@ def main():
     def frame():
         pt.mark_dirty()  # each step is a fresh 8-spp frame from seed 0
         pt.render(args.spp, stream=stream)
-        if gather is not None:
-            gather.gather(pt.buffers.get(FINAL_RESULT))
+        if gather is not None:  # overlapped with the next frame on a side stream (dist.FrameGather)
+            gather.gather_async(pt.buffers.get(FINAL_RESULT), stream)
 
     # one instrumented frame for the traversal byte counts (untimed)
     pt.mark_dirty()

@@ -7,6 +7,8 @@ Tile t (32x32, row-major) belongs to rank t % world (pupil_pt_local_pixels).
 Once per frame every rank's compact tile radiance is gathered to rank 0 over
 RCCL (backend "nccl") and scattered into the full image — one collective,
 ~4 MB per rank at 1080p/8 GPUs.  Results are bit-identical to one GPU.
+gather_async() runs the snapshot, the collective and the scatter on a side HIP
+stream, so frame k's gather overlaps frame k+1's rendering.
 """
 from __future__ import annotations
 
@@ -42,6 +44,7 @@ class FrameGather:
         self.recv = [torch.zeros_like(self.send) for _ in range(world)] if rank == 0 else None
         self.full = (torch.zeros((width * height, channels), dtype=torch.float32, device=device)
                      if rank == 0 else None)
+        self._side = None  # gather_async's side stream (created on first use)
 
     def gather(self, local):
         import torch.distributed as dist
@@ -53,3 +56,40 @@ class FrameGather:
                 self.full.index_copy_(0, self.maps[r], self.recv[r][: self.counts[r]])
             return self.full
         return None
+
+    def gather_async(self, local, stream=None):
+        """gather() overlapped with the caller's next frame (GPU tensors).
+
+        A side stream waits for `stream`'s work so far, snapshots `local` into the
+        send buffer, runs the collective and (rank 0) the scatter into the full
+        image; `stream` waits only for the snapshot, so the next frame may start
+        at once and overwrite `local`.  The full image is valid once the side
+        stream has drained (wait() or torch.cuda.synchronize()).  Side-stream work
+        of consecutive calls runs in call order, so the send/recv buffers are
+        reused safely.  CPU tensors (gloo) take the synchronous path."""
+        import torch
+        import torch.distributed as dist
+
+        if local.device.type != "cuda":
+            return self.gather(local)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=local.device)
+            self._copied = torch.cuda.Event()
+        stream = stream if stream is not None else torch.cuda.current_stream(local.device)
+        ready = torch.cuda.Event()
+        ready.record(stream)
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            self.send[: self.n_local].copy_(local)
+            self._copied.record(self._side)
+            dist.gather(self.send, self.recv, dst=0)
+            if self.rank == 0:
+                for r in range(self.world):
+                    self.full.index_copy_(0, self.maps[r], self.recv[r][: self.counts[r]])
+        stream.wait_event(self._copied)
+        return self.full if self.rank == 0 else None
+
+    def wait(self):
+        """Block the host until every gather_async() so far has completed."""
+        if self._side is not None:
+            self._side.synchronize()

@@ -31,7 +31,9 @@ def _worker(rank, world, port, w, h, tile, out_path):
     pix = local_pixels(w, h, tile, rank, world)
     local = torch.from_numpy(np.stack([pix, pix * 2, pix * 3, np.ones_like(pix)], 1).astype(np.float32))
     full = g.gather(local)
+    again = g.gather_async(local)  # CPU tensors: the synchronous path, same result
     if rank == 0:
+        assert torch.equal(full, again)
         np.save(out_path, full.numpy())
     dist.barrier()
     dist.destroy_process_group()
@@ -60,3 +62,27 @@ def test_tiles_partition_image_and_balance(world):
     assert (seen == 1).all()
     # interleaved tiles: every rank within 2 tiles of the mean
     assert max(counts) - min(counts) <= 2 * tile * tile
+
+
+@pytest.mark.gpu
+def test_gather_async_on_gpu_single_rank():
+    """The overlapped gather's stream/event plumbing over RCCL (one rank): the side
+    stream snapshots the tile buffer, the caller's stream may overwrite it at once,
+    and the gathered image is the snapshot."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dev = torch.device("cuda:0")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        w, h, tile = 96, 64, 32
+        g = FrameGather(w, h, tile, 0, 1, dev)
+        s = torch.cuda.current_stream(dev)
+        pix = torch.arange(w * h, dtype=torch.float32, device=dev)
+        local = torch.stack([pix, 2 * pix, 3 * pix, torch.ones_like(pix)], 1)
+        full = g.gather_async(local, s)
+        local.fill_(-1.0)  # the next frame overwrites the tile buffer on the render stream
+        torch.cuda.synchronize(dev)
+        assert torch.equal(full[:, 1], 2 * pix)
+        assert torch.equal(full[:, 3], torch.ones_like(pix))
+    finally:
+        dist.destroy_process_group()
