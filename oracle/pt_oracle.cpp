@@ -1090,19 +1090,24 @@ bool HitTriangle(const Ray &r, const Prim &p, float tmin, float tmax, float &t, 
     return true;
 }
 
+// Unit sphere in object space, closest-approach discriminant (Ray Tracing Gems
+// ch. 7), the same arithmetic as csrc/pt_trace.h intersect_unit_sphere.
 bool HitSphere(const Instance &in, const Ray &r, float tmin, float tmax, float &t) {
-    const float3 oo = XformPoint(in.to_object, r.o);
+    const float3 f = XformPoint(in.to_object, r.o);
     const float3 od = XformVector(in.to_object, r.d);
-    const float a = dot(od, od), b = dot(oo, od), c = dot(oo, oo) - 1.f;
-    const float disc = b * b - a * c;
+    const float a = dot(od, od);
+    const float bp = -dot(f, od);
+    const float3 l = f + od * (bp / a);
+    const float disc = a * (1.f - dot(l, l));
     if (disc < 0.f) return false;
-    const float s = sqrtf(disc);
-    const float t0 = (-b - s) / a;
+    const float c = dot(f, f) - 1.f;
+    const float q = bp + std::copysign(sqrtf(disc), bp);
+    const float r0 = c / q, r1 = q / a;
+    const float t0 = std::fmin(r0, r1), t1 = std::fmax(r0, r1);
     if (t0 >= tmin && t0 <= tmax) {
         t = t0;
         return true;
     }
-    const float t1 = (-b + s) / a;
     if (t1 >= tmin && t1 <= tmax) {
         t = t1;
         return true;
@@ -1373,9 +1378,9 @@ bool LoadScene(const pupil_scene_desc &d, Scene &sc) {
             Box b;
             if (p.sphere) {
                 const float *m = in.to_world;
-                const float ex = std::sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.0001f;
-                const float ey = std::sqrt(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.0001f;
-                const float ez = std::sqrt(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.0001f;
+                const float ex = std::sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.001f;
+                const float ey = std::sqrt(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.001f;
+                const float ez = std::sqrt(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.001f;
                 b.grow(make_float3(m[3] - ex, m[7] - ey, m[11] - ez));
                 b.grow(make_float3(m[3] + ex, m[7] + ey, m[11] + ez));
                 p.v0 = p.v1 = p.v2 = make_float3(m[3], m[7], m[11]);

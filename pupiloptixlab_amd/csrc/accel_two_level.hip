@@ -47,9 +47,9 @@ __global__ __launch_bounds__(kBlock) void k_inst_bounds(const DevInstance *insts
     if (in.kind == PUPIL_SHAPE_SPHERE) {
         if (threadIdx.x == 0) {
             const float *m = in.to_world;
-            const float ex = sqrtf(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.0001f;
-            const float ey = sqrtf(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.0001f;
-            const float ez = sqrtf(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.0001f;
+            const float ex = sqrtf(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.001f;
+            const float ey = sqrtf(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.001f;
+            const float ez = sqrtf(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.001f;
             o[0] = m[3] - ex;
             o[1] = m[7] - ey;
             o[2] = m[11] - ez;

@@ -55,9 +55,9 @@ __global__ void k_prim_setup(BvhBuildInput in, float4 *recs, Aabb *boxes) {
         const float *m = inst.to_world;
         const vec3 c = v3(m[3], m[7], m[11]);
         // exact extents of an affinely transformed unit sphere, padded
-        const float ex = sqrtf(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.0001f;
-        const float ey = sqrtf(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.0001f;
-        const float ez = sqrtf(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.0001f;
+        const float ex = sqrtf(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.001f;
+        const float ey = sqrtf(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.001f;
+        const float ez = sqrtf(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.001f;
         b.lo[0] = c.x - ex; b.lo[1] = c.y - ey; b.lo[2] = c.z - ez;
         b.hi[0] = c.x + ex; b.hi[1] = c.y + ey; b.hi[2] = c.z + ez;
         recs[3 * i + 0] = make_float4(c.x, c.y, c.z, __uint_as_float(i | kPrimSphereBit));
