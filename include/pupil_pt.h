@@ -260,6 +260,41 @@ int pupil_debug_math(int device, uint32_t n, const float *x, const float *y2, fl
 enum { PUPIL_IMAGE_AUTO = 0, PUPIL_IMAGE_EXR = 1, PUPIL_IMAGE_HDR = 2, PUPIL_IMAGE_PFM = 3 };
 int pupil_image_save(const char *path, uint32_t width, uint32_t height, const float *rgba, uint32_t format);
 
+/* ---- denoiser (substitute for optix::Denoiser, framework/optix/denoiser.h:7-66) ----
+ * The OptiX AI denoiser has no ROCm equivalent; this is an edge-avoiding
+ * a-trous wavelet filter (Dammertz et al. 2010): five passes of a 5x5 B3-spline
+ * kernel at strides 1, 2, 4, 8, 16, each tap weighted by colour, normal and
+ * albedo similarity.  Mode bits and Execute's data follow the reference:
+ * UseAlbedo / UseNormal select the guides, UseTemporal blends with prev_output
+ * (no motion vectors: static camera), Tiled is accepted (the whole frame is
+ * filtered at once), ApplyToAOV and UseUpscale2X return PUPIL_ERR_UNSUPPORTED.
+ * Buffers are device pointers: input/output/prev_output float4 per pixel,
+ * albedo/normal float3 per pixel (the "albedo"/"normal" AOVs). */
+enum {
+    PUPIL_DENOISE_USE_ALBEDO = 1,
+    PUPIL_DENOISE_USE_NORMAL = 1 << 1,
+    PUPIL_DENOISE_APPLY_TO_AOV = 1 << 2,
+    PUPIL_DENOISE_USE_TEMPORAL = 1 << 3,
+    PUPIL_DENOISE_USE_UPSCALE_2X = 1 << 4,
+    PUPIL_DENOISE_TILED = 1 << 5
+};
+typedef struct pupil_denoise_data {
+    const void *input;        /* float4 */
+    void *output;             /* float4 (may equal input) */
+    const void *prev_output;  /* float4, UseTemporal only (NULL: first frame) */
+    const void *albedo;       /* float3, UseAlbedo */
+    const void *normal;       /* float3, UseNormal */
+    const void *motion_vector; /* unused (must be NULL) */
+} pupil_denoise_data;
+typedef struct pupil_denoiser pupil_denoiser;
+/* Denoiser(mode, stream) (denoiser.h:20-21) */
+int pupil_denoiser_create(int device, uint32_t mode, pupil_denoiser **out);
+/* SetMode / Setup(w, h) (denoiser.h:24-25); sigma_color scales the colour edge-stopping term (0 = 1.0) */
+int pupil_denoiser_setup(pupil_denoiser *d, uint32_t mode, uint32_t width, uint32_t height, float sigma_color);
+/* Execute(ExecutionData) (denoiser.h:31-40); asynchronous on hip_stream */
+int pupil_denoiser_execute(pupil_denoiser *d, const pupil_denoise_data *data, void *hip_stream);
+void pupil_denoiser_destroy(pupil_denoiser *d);
+
 /* ---- host world (the reference's resource::Scene + world::World, C++ inside) ---- */
 typedef struct pupil_world pupil_world;
 

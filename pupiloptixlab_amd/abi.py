@@ -92,6 +92,15 @@ class Counters(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+DENOISE_USE_ALBEDO, DENOISE_USE_NORMAL, DENOISE_APPLY_TO_AOV = 1, 2, 4
+DENOISE_USE_TEMPORAL, DENOISE_USE_UPSCALE_2X, DENOISE_TILED = 8, 16, 32
+
+
+class DenoiseData(C.Structure):
+    _fields_ = [("input", C.c_void_p), ("output", C.c_void_p), ("prev_output", C.c_void_p),
+                ("albedo", C.c_void_p), ("normal", C.c_void_p), ("motion_vector", C.c_void_p)]
+
+
 # name -> (restype, argtypes); every entry is declared in include/pupil_pt.h
 SIGNATURES = {
     "pupil_last_error": (C.c_char_p, []),
@@ -121,6 +130,10 @@ SIGNATURES = {
     "pupil_world_set_instance_transform": (C.c_int, [C.c_void_p, C.c_uint32, f32p]),
     "pupil_world_get_desc": (C.c_int, [C.c_void_p, C.POINTER(SceneDesc)]),
     "pupil_world_destroy": (None, [C.c_void_p]),
+    "pupil_denoiser_create": (C.c_int, [C.c_int, C.c_uint32, C.POINTER(C.c_void_p)]),
+    "pupil_denoiser_setup": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_float]),
+    "pupil_denoiser_execute": (C.c_int, [C.c_void_p, C.POINTER(DenoiseData), C.c_void_p]),
+    "pupil_denoiser_destroy": (None, [C.c_void_p]),
 }
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
