@@ -10,6 +10,7 @@
 #include <memory>
 #include <vector>
 
+#include "pupil/denoiser.h"
 #include "pupil/framework.h"
 #include "pupil/pt_pass.h"
 
@@ -32,8 +33,20 @@ int main(int argc, char **argv) {
         } else {
             system->Run((uint32_t)frames);
             pt_pass->Inspector();
-            auto *buf = Pupil::BufferManager::instance()->GetBuffer(Pupil::BufferManager::DEFAULT_FINAL_RESULT_BUFFER_NAME);
+            auto *bm = Pupil::BufferManager::instance();
+            auto *buf = bm->GetBuffer(Pupil::BufferManager::DEFAULT_FINAL_RESULT_BUFFER_NAME);
             const int w = system->GetWorld()->scene->sensor.film.w, h = system->GetWorld()->scene->sensor.film.h;
+            const char *dn = std::getenv("PUPIL_DENOISE");  // optix::Denoiser substitute on the final result
+            if (buf && dn && std::atoi(dn)) {
+                Pupil::optix::Denoiser denoiser(Pupil::optix::Denoiser::UseAlbedo | Pupil::optix::Denoiser::UseNormal);
+                denoiser.Setup((unsigned)w, (unsigned)h);
+                Pupil::optix::Denoiser::ExecutionData data;
+                data.input = buf->cuda_ptr;
+                data.output = buf->cuda_ptr;
+                data.albedo = bm->GetBuffer("albedo")->cuda_ptr;
+                data.normal = bm->GetBuffer("normal")->cuda_ptr;
+                if (!denoiser.Execute(data) || hipDeviceSynchronize() != hipSuccess) rc = 1;
+            }
             std::vector<float> host(4 * (size_t)w * h);
             if (!buf || hipMemcpy(host.data(), buf->cuda_ptr, host.size() * sizeof(float), hipMemcpyDeviceToHost) !=
                             hipSuccess) {

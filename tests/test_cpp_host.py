@@ -69,3 +69,40 @@ def test_example_matches_python_pass_and_oracle():
     assert np.array_equal(img, py)
     ref = oracle.OracleScene(desc).render(spp=4)["accum"][:, :3]
     assert np.array_equal(img, ref)
+
+
+@pytest.mark.gpu
+def test_example_denoised_output_matches_python_denoiser():
+    """PUPIL_DENOISE=1: the example runs Pupil::optix::Denoiser (albedo + normal guides) on
+    "final result" before saving; the image equals the Python Denoiser on the same frame."""
+    _built()
+    import torch
+    from pupiloptixlab_amd import World, scenes
+    from pupiloptixlab_amd.denoiser import Denoiser
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    os.makedirs(TMP, exist_ok=True)
+    xml = scenes.cornell_xml(os.path.join(TMP, "cb_cpp_dn.xml"), 64, 48, 4)
+    out = os.path.join(TMP, "cb_cpp_dn.pfm")
+    r = subprocess.run([EXE, xml, "4", out], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PUPIL_DENOISE="1"))
+    assert r.returncode == 0, r.stderr
+    img = _read_pfm(out).reshape(-1, 3)
+
+    desc = World().load_scene(xml).desc()
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    for _ in range(4):
+        pt.on_run()
+    final = pt.buffers.get("final result")
+    dn = Denoiser(Denoiser.USE_ALBEDO | Denoiser.USE_NORMAL)
+    dn.setup(64, 48, 0.5)
+    res = torch.empty_like(final)
+    dn.execute(final, res, albedo=pt.buffers.get("albedo"), normal=pt.buffers.get("normal"))
+    torch.cuda.synchronize()
+    py = res.cpu().numpy()[:, :3]
+    noisy = final.cpu().numpy()[:, :3]
+    pt.close_engine()
+    dn.close()
+    assert np.array_equal(img, py)
+    assert not np.array_equal(img, noisy)
