@@ -19,6 +19,7 @@
 // flags (bit b puts the path in bin b when the key's bounce tag, bits 2..7,
 // equals `shift`; a path can be in several bins).
 #include <algorithm>
+#include <cstdlib>
 
 #include "pt_kernels.h"
 
@@ -30,8 +31,18 @@ constexpr int kPartBlock = 256;               // 4 waves
 constexpr uint32_t kPartMaxRounds = 64;       // rounds of 64 paths per wave
 constexpr uint32_t kPartTargetBlocks = 2048;
 
+// launch-size target, <= kPartTargetBlocks (PUPIL_PART_BLOCKS, A/B: fewer blocks shorten the scan)
+uint32_t part_target() {
+    static const uint32_t t = [] {
+        const char *e = std::getenv("PUPIL_PART_BLOCKS");
+        const int v = e ? std::atoi(e) : (int)kPartTargetBlocks;
+        return (uint32_t)std::min((int)kPartTargetBlocks, std::max(64, v));
+    }();
+    return t;
+}
 uint32_t part_rounds(uint32_t n) {
-    const uint32_t r = (uint32_t)(((uint64_t)n + 256ull * kPartTargetBlocks - 1) / (256ull * kPartTargetBlocks));
+    const uint32_t tb = part_target();
+    const uint32_t r = (uint32_t)(((uint64_t)n + 256ull * tb - 1) / (256ull * tb));
     return std::max(1u, std::min(kPartMaxRounds, r));
 }
 uint32_t part_blocks(uint32_t n) {
