@@ -408,3 +408,33 @@ def test_env_map_and_bitmap_textures_parity():
     assert exact == 160 * 120
     for k in ("albedo", "normal"):
         assert np.array_equal(gpu[k], ref[k])
+
+
+def test_render_from_another_thread():
+    """SURVEY §8(b) threading: PTPass::OnRun runs on a render thread other than the one that
+    created the engine (system.cpp:93-106); every call sets its HIP device, so a render issued
+    from a worker thread equals one issued from the creating thread."""
+    import threading
+
+    import torch
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    desc = _cornell(48).desc()
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    pt.render(2)
+    torch.cuda.synchronize()
+    main = pt.buffers.get("pt accum buffer").cpu().numpy()
+    out = {}
+
+    def worker():
+        pt.mark_dirty()
+        pt.render(2)
+        torch.cuda.synchronize()
+        out["img"] = pt.buffers.get("pt accum buffer").cpu().numpy()
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join(timeout=60)
+    pt.close_engine()
+    assert "img" in out and np.array_equal(out["img"], main)
