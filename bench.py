@@ -51,6 +51,7 @@ def parse():
                     help="CPU baseline renders every k-th pixel (default: full frame for configs 3/4, 1/16 for 5)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--save", default="", help="write the frame as PNG (rank 0)")
+    ap.add_argument("--dump", default="", help="write the full float32 frame as .npy (rank 0, after the timed steps)")
     args = ap.parse_args()
     defaults = {3: (125, 1920, 1080, 8, 4, 1), 4: (500, 1920, 1080, 8, 4, 1), 5: (125, 3840, 2160, 16, 6, 16)}
     sph, w, h, spp, depth, stride = defaults[args.config]
@@ -71,8 +72,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank path on a box with fewer GPUs: PUPIL_BENCH_DEVICES=k maps
+    # local rank r to GPU r % k (never set by the driver's runs: one rank per GPU)
+    if os.environ.get("PUPIL_BENCH_DEVICES"):
+        local_rank %= max(1, int(os.environ["PUPIL_BENCH_DEVICES"]))
+    backend = os.environ.get("PUPIL_BENCH_BACKEND", "nccl")  # gloo: rehearsal with several ranks per GPU
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local_rank)
     dev = torch.device(f"cuda:{local_rank}")
 
@@ -143,7 +152,8 @@ def main():
     ext_ms, trace_ms, shade_ms = st["extend_ms"], st["trace_ms"], st["shade_ms"]
     trace_launches = st["trace_launches"]
 
-    t = torch.tensor([elapsed, float(rays_local), trace_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, float(rays_local), trace_ms], dtype=torch.float64,
+                     device=dev if backend == "nccl" else "cpu")
     if world > 1:
         t_max = t.clone()
         dist.all_reduce(t_max[0:1], op=dist.ReduceOp.MAX)
@@ -173,6 +183,9 @@ def main():
         cpu = cpu_baseline(desc, args)
 
     if rank == 0:
+        if args.dump:
+            full = gather.full if gather is not None else pt.buffers.get(FINAL_RESULT)
+            np.save(args.dump, full.cpu().numpy())
         if args.save:
             from tools import imgio
 

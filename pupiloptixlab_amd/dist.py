@@ -72,6 +72,17 @@ class FrameGather:
 
         if local.device.type != "cuda":
             return self.gather(local)
+        if dist.get_backend() != "nccl":  # rehearsal over gloo: stage through host memory, synchronously
+            host = FrameGather.__new__(FrameGather)
+            host.__dict__.update(self.__dict__)
+            host.send, host.maps = self.send.cpu(), [m.cpu() for m in self.maps]
+            host.recv = [r.cpu() for r in self.recv] if self.recv is not None else None
+            host.full = self.full.cpu() if self.full is not None else None
+            full = host.gather(local.cpu())
+            if self.rank == 0:
+                self.full.copy_(full)
+                return self.full
+            return None
         if self._side is None:
             self._side = torch.cuda.Stream(device=local.device)
             self._copied = torch.cuda.Event()
