@@ -9,7 +9,7 @@
 namespace pupil {
 
 constexpr int kTraceBlock = 128;
-constexpr int kTraceWavesPerSimd = 6;  // persistent BVH4 kernels: occupancy target (<= 80 VGPRs)
+constexpr int kTraceWavesPerSimd = 7;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8: 2 % slower)
 constexpr int kTraceWavesPerSimdTL = 4;  // two-level variant (<= 128 VGPRs)
 constexpr int kStackLds = 32;   // per-thread LDS stack entries
 constexpr int kStackOvf = 96;   // per-thread global overflow entries
