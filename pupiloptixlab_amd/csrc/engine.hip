@@ -92,7 +92,7 @@ struct pupil_pt {
     TwoLevelAccel tl{};
     uint32_t width = 0, height = 0, max_depth = 1;
     uint32_t num_prims = 0;
-    uint32_t leaf_size = 3;  // primitives per BVH leaf (PUPIL_LEAF_SIZE)
+    uint32_t leaf_size = 2;  // primitives per BVH leaf (PUPIL_LEAF_SIZE)
     bool mixed_trace = true;  // one persistent launch per bounce for shadow + extension rays (PUPIL_MIXED)
     double build_ms = 0.0;
     // path state / queues (grown on demand)
@@ -471,7 +471,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     pt->d_insts = d_insts;
     pt->d_mats = d_mats;
     pt->d_prim_inst = d_prim_inst;
-    pt->leaf_size = 3u;
+    pt->leaf_size = 2u;  // with the 7-wave traversal: 2 beats 3 by 2 %, 1 and 4 are slower (config 4)
     if (const char *ls = std::getenv("PUPIL_LEAF_SIZE")) pt->leaf_size = (uint32_t)std::min(8, std::max(1, std::atoi(ls)));
     // Acceleration structure (replaces the GAS + IAS builds): one flattened BVH over
     // world-space primitives (default: on config 5 it traces 3.2x faster than the
@@ -550,7 +550,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (pt->two_level && sc.trace_refill == 0) sc.trace_refill = 24;  // two-level: persistent BVH4 kernels only
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
-    sc.trace_node_min = 4;
+    sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     sc.prim_inst = d_prim_inst;
     sc.instances = d_insts;
