@@ -638,8 +638,21 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         const unsigned long long idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
         if (!drained && n_idle >= job.refill) {
-            const uint32_t lo = (uint32_t)((uint64_t)count * shard / kWorkShards);
-            const uint32_t len = (uint32_t)((uint64_t)count * (shard + 1) / kWorkShards) - lo;
+            // chunk `shard`: list positions [lo, lo + len).  Mixed launches cut the
+            // extension and the shadow list separately and give each chunk its
+            // extension share first, so every chunk ends on (cheaper) shadow rays
+            // and the launch tail is not made of closest-hit traversals.
+            uint32_t lo, len, len_e = 0, lo_s = 0;
+            if (MODE == kModeMixed) {
+                const uint32_t n_sh = count - n_next;
+                lo = (uint32_t)((uint64_t)n_next * shard / kWorkShards);
+                len_e = (uint32_t)((uint64_t)n_next * (shard + 1) / kWorkShards) - lo;
+                lo_s = n_next + (uint32_t)((uint64_t)n_sh * shard / kWorkShards);
+                len = len_e + (n_next + (uint32_t)((uint64_t)n_sh * (shard + 1) / kWorkShards) - lo_s);
+            } else {
+                lo = (uint32_t)((uint64_t)count * shard / kWorkShards);
+                len = (uint32_t)((uint64_t)count * (shard + 1) / kWorkShards) - lo;
+            }
             uint32_t base = 0;
             if (lane_id() == 0) base = atomicAdd(job.work + shard * kWorkStride, n_idle);
             base = __shfl(base, 0);
@@ -653,7 +666,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             }
             if (!active) {
                 const uint32_t k = base + (uint32_t)__popcll(idle & lanemask_lt());
-                const uint32_t i = lo + k;
+                const uint32_t i = MODE == kModeMixed && k >= len_e ? lo_s + (k - len_e) : lo + k;
                 if (k < len) {
                     float4 o, d;
                     if (MODE == kModeExtend) {
