@@ -834,7 +834,7 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
     hipError_t e = hipMalloc((void **)&d_out, sizeof(float) * 4 * (size_t)n);
     if (e == hipSuccess) e = hipMemcpy(d_rays, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        e = hipMemsetAsync(pt->q.work + kWorkRays, 0, kWorkShards * kWorkStride * sizeof(uint32_t), pt->own_stream);
+        e = hipMemsetAsync(pt->q.work + kWorkRays, 0, kWorkKind * sizeof(uint32_t), pt->own_stream);
         if (e == hipSuccess)
             launch_trace_debug(pt->sc, d_rays, d_out, n, any_hit, pt->ovf, pt->ovf_threads, pt->q.work + kWorkRays,
                                pt->own_stream);

@@ -47,9 +47,10 @@ constexpr int kPartMaxBins = 9;
 // counts[] slots
 constexpr uint32_t kCntNext = 9, kCntShadow = 10;                      // queue lengths
 // persistent-kernel work counters: per kind kWorkShards dequeue heads (one per
-// XCD) and one exit counter, each on its own 128-B line.  Zero at allocation;
-// the last wave of every persistent launch puts them back to zero.
-constexpr uint32_t kWorkShards = 8, kWorkStride = 32, kWorkKind = (kWorkShards + 1) * kWorkStride;
+// XCD), one final exit counter and kWorkShards exit sub-counters, each on its
+// own 128-B line.  Zero at allocation; the last wave of every persistent launch
+// puts them back to zero.
+constexpr uint32_t kWorkShards = 8, kWorkStride = 32, kWorkKind = (2 * kWorkShards + 1) * kWorkStride;
 constexpr uint32_t kWorkExtend = 0, kWorkShadow = kWorkKind, kWorkRays = 2 * kWorkKind;
 constexpr uint32_t kWorkSlots = 3 * kWorkKind;
 constexpr uint32_t kStartBins = 16;                                    // [16..24] material bin starts

@@ -486,7 +486,7 @@ struct TraceJob {
     const uint32_t *queue;      // extend: path ids (null = identity)
     const uint32_t *count_ptr;  // device count (null = static_count)
     uint32_t static_count;
-    uint32_t *work;             // kWorkShards work heads + exit counter (stride kWorkStride), zero at launch
+    uint32_t *work;             // kWorkKind counters: heads, final and sub exit counters (stride kWorkStride), zero at launch
     uint32_t refill;            // refill when at least this many lanes are idle (1..64)
     uint32_t node_min;          // node phase ends when fewer lanes than this still need a node (>= 1)
     const float *rays;          // kModeRays: 8 floats per ray (o, d, tmin, tmax)
@@ -857,11 +857,18 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     }
     flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
     if (MODE == kModeMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
-    // the last wave out resets the heads for the next launch (no memset per launch)
+    // the last wave out resets the counters for the next launch (no memset per
+    // launch).  Waves count out on kWorkShards sub-counters (blockIdx % shards),
+    // the last of each sub-counter on the final one: the exit burst at the end
+    // of a launch is spread over kWorkShards addresses instead of serialised
+    // on one (~88 atomics/us per address).
     if (lane_id() == 0) {
-        const uint32_t waves = gridDim.x * (blockDim.x / 64u);
-        if (atomicAdd(job.work + kWorkShards * kWorkStride, 1u) == waves - 1u)
-            for (uint32_t k = 0; k <= kWorkShards; k++) atomicExch(job.work + k * kWorkStride, 0u);
+        const uint32_t sub = blockIdx.x % kWorkShards;
+        const uint32_t groups = min(gridDim.x, kWorkShards);
+        const uint32_t sub_waves = (gridDim.x - sub + kWorkShards - 1u) / kWorkShards * (blockDim.x / 64u);
+        if (atomicAdd(job.work + (kWorkShards + 1u + sub) * kWorkStride, 1u) == sub_waves - 1u &&
+            atomicAdd(job.work + kWorkShards * kWorkStride, 1u) == groups - 1u)
+            for (uint32_t k = 0; k < 2u * kWorkShards + 1u; k++) atomicExch(job.work + k * kWorkStride, 0u);
     }
     if (STATS) {
         for (int k = 0; k < 6; k++) {
