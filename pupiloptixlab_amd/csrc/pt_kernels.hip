@@ -1293,8 +1293,15 @@ __global__ void k_debug_math(const float *x, const float *y2, float *out, uint32
 }  // namespace
 
 // Persistent grid: exactly the resident capacity (CUs x 4 SIMDs x waves per SIMD).
+// PUPIL_TRACE_GRID_WAVES (A/B knob): fewer waves per SIMD in the grid than the
+// kernel's occupancy allows.
 static uint32_t trace4_blocks(const DeviceScene &sc, uint32_t ovf_threads) {
-    const uint32_t waves = sc.two_level ? kTraceWavesPerSimdTL : kTraceWavesPerSimd;
+    static const int forced = [] {
+        const char *e = std::getenv("PUPIL_TRACE_GRID_WAVES");
+        return e ? std::max(1, std::atoi(e)) : 0;
+    }();
+    const uint32_t occ = sc.two_level ? kTraceWavesPerSimdTL : kTraceWavesPerSimd;
+    const uint32_t waves = forced ? std::min(occ, (uint32_t)forced) : occ;
     const uint32_t resident = sc.num_cus * 4u * waves / (kTraceBlock / 64u);
     return std::min(ovf_threads / kTraceBlock, std::max(1u, resident));
 }
