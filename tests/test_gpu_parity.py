@@ -127,6 +127,26 @@ def test_cornell_parity_config1():
         (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
 
 
+def test_config1_cornellbox_named_size():
+    """BASELINE config 1 exactly as named: the reference's own cornellbox.xml (committed
+    numeric fixture), 256x256, 1 spp, max depth 4, seed 0 (`main.cu:36-194`).  Every pixel,
+    the AOVs and the ray counts are bit-identical to the oracle."""
+    from pupiloptixlab_amd import scene_io
+
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_scenes", "cornellbox.npz")
+    d = scene_io.LoadedScene(gold).resized(256, 256)
+    assert d.max_depth == 4
+    gpu = render_gpu(d, 1)
+    ref = oracle.OracleScene(d).render(spp=1)
+    exact = compare(gpu, ref, "config1-cornellbox256x1")
+    assert exact == 256 * 256
+    assert np.array_equal(gpu["pt accum buffer"].view(np.uint32), ref["accum"].view(np.uint32))
+    assert np.array_equal(gpu["albedo"], ref["albedo"]) and np.array_equal(gpu["normal"], ref["normal"])
+    s, rs = gpu["stats"], ref["stats"]
+    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
+        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
+
+
 @pytest.mark.parametrize("accel", ["flat", "two_level"])
 def test_materials_parity_config2(accel, monkeypatch):
     """Config 2 (all seven BSDFs, spheres + boxes) at 192^2, 8 spp, depth 6; one flattened
