@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1 only)")
     ap.add_argument("--cpu-sample-stride", type=int, default=None,
                     help="CPU baseline renders every k-th pixel (default: full frame for configs 3/4, 1/16 for 5)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every CPU this process may run on, capped by the cgroup quota)")
     ap.add_argument("--save", default="", help="write the frame as PNG (rank 0)")
     ap.add_argument("--dump", default="", help="write the full float32 frame as .npy (rank 0, after the timed steps)")
     args = ap.parse_args()
@@ -115,11 +116,13 @@ def main():
         gather = FrameGather(args.width, args.height, args.tile, rank, world, dev)
         assert gather.n_local == n_local
 
+    handles = []
+
     def frame():
         pt.mark_dirty()  # each step is a fresh 8-spp frame from seed 0
         pt.render(args.spp, stream=stream)
         if gather is not None:  # overlapped with the next frame on a side stream (dist.FrameGather)
-            gather.gather_async(pt.buffers.get(FINAL_RESULT), stream)
+            handles.append(gather.gather_async(pt.buffers.get(FINAL_RESULT), stream))
 
     # one instrumented frame for the traversal byte counts (untimed)
     pt.mark_dirty()
@@ -166,30 +169,25 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     mrays = rays_total / elapsed / 1e6
     rays_frame_local = st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"]
-    # roofline of the dominant kernel, the persistent BVH4 traversal k_trace4
-    # (per frame: the primary extend launch, then one launch per bounce over
-    # the concatenated extension + shadow lists): algorithmic bytes per SURVEY.md
-    # §8(d) = 32 B ray + 16 B hit + 64 B per node visit + 48 B per primitive
-    # test, counted in the instrumented frame, per launch; divided by the
-    # average traversal launch time measured with HIP events on the render
-    # stream in the last timed frame
-    per_launch_bytes = st_bytes["trace_bytes"] / max(1, st_bytes["trace_launches"])
-    per_launch_ms = trace_ms / max(1, trace_launches)
-    achieved_gbs = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
-    traffic = pmc_traffic(args)
-
+    # roofline of the dominant kernel, the persistent BVH4 traversal k_trace4 (per
+    # frame: the primary extend launch, then one launch per bounce over the
+    # concatenated extension + shadow lists).  Three ceilings are evaluated and the
+    # binding (highest) one is reported: dependent node gathers (live node-visit
+    # rate / the gather ceiling measured on this box by build/ubench_gather), VALU
+    # issue and HBM bytes (both from the committed PMC passes of this config).
+    roof = roofline(args, st_bytes, trace_ms, trace_launches) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        cpu = cpu_baseline(desc, args)
+        cpu = cpu_baseline(desc, args, pt)
 
     if rank == 0:
         if args.dump:
-            full = gather.full if gather is not None else pt.buffers.get(FINAL_RESULT)
+            full = handles[-1].synchronize() if gather is not None else pt.buffers.get(FINAL_RESULT)
             np.save(args.dump, full.cpu().numpy())
         if args.save:
             from tools import imgio
 
-            img = (gather.full if gather is not None else pt.buffers.get(FINAL_RESULT)).cpu().numpy()
+            img = (handles[-1].synchronize() if gather is not None else pt.buffers.get(FINAL_RESULT)).cpu().numpy()
             imgio.save_render(args.save, img.reshape(args.height, args.width, 4))
         out = {
             "metric": "Mrays/sec + ms/frame, 1M-tri scene @1920x1080 8spp; 1/2/4/8-GPU scaling",
@@ -210,6 +208,14 @@ def main():
                                     f"{args.width}x{args.height}, {args.spp} spp, max_depth {args.max_depth}"),
                        "frame": f"{args.spp} x PTPass::OnRun", "parallelism": f"tiles{args.tile}x{world}",
                        "rays_per_frame": rays_total / args.steps,
+                       # shadow rays the reference would trace (one per loop iteration past RR,
+                       # main.cu:119-123); the engine and the oracle trace one only when the
+                       # contribution is non-zero (radiance-equivalent: Eval draws no random
+                       # numbers, optix_material.h:57-62), so value counts traced rays only
+                       "shadow_rays_traced": int(st_bytes["shadow_rays"]),
+                       "shadow_rays_reference_count": int(st_bytes["shadow_rays_reference"]),
+                       "rays_per_frame_reference_count": int(st_bytes["primary_rays"] + st_bytes["extension_rays"] +
+                                                             st_bytes["shadow_rays_reference"]),
                        "path_samples_per_s": round(args.width * args.height * args.spp / (ms_per_step * 1e-3), 1),
                        "bvh_build_ms": round(st_bytes["build_ms"], 3),
                        "bvh_nodes": int(st_bytes["bvh_nodes"]),
@@ -226,19 +232,7 @@ def main():
                        "stage_ms_per_frame": {"primary_extend": round(ext_ms, 3),
                                               "bounce_trace": round(trace_ms - ext_ms, 3),
                                               "shade": round(shade_ms, 3)}},
-            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_trace4 (persistent BVH4 traversal, all launches: primary extend + "
-                                   "per-bounce extension+shadow)",
-                         "bytes_per_launch": round(per_launch_bytes, 1),
-                         "ms_per_launch": round(per_launch_ms, 4),
-                         # the BVH (15 MB of nodes + 48 MB of primitives) is resident in the 256 MB
-                         # Infinity Cache, so algorithmic node/primitive bytes can exceed the HBM peak;
-                         # the PMC-measured L2->fabric bytes give the bandwidth actually drawn
-                         "traffic_gbs": (round(traffic / (per_launch_ms * 1e-3) / 1e9, 1)
-                                         if traffic and per_launch_ms > 0 else None),
-                         "traffic_frac": (round(traffic / (per_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                          if traffic and per_launch_ms > 0 else None)},
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
@@ -246,38 +240,150 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(args):
-    """roofline.traffic: L2->fabric bytes per extend launch measured by the PMC
-    passes of this same command (tools/gpu_pmc.sh -> tools/pmc_summary.py
-    --json), committed as profiles/pmc_extend.json; null when absent or taken
-    on another configuration."""
-    path = os.path.join(HERE, "profiles", "pmc_extend.json")
-    default_cfg = args.config == 4 and \
-        (args.spheres, args.width, args.height, args.spp, args.max_depth) == (500, 1920, 1080, 8, 4)
-    if not default_cfg or not os.path.exists(path):
+def default_config(args):
+    defaults = {3: (125, 1920, 1080, 8, 4), 4: (500, 1920, 1080, 8, 4), 5: (125, 3840, 2160, 16, 6)}
+    return (args.spheres, args.width, args.height, args.spp, args.max_depth) == defaults[args.config]
+
+
+def pmc_record(args):
+    """Per-launch PMC figures of k_trace4 for this config (tools/gpu_pmc.sh ->
+    tools/pmc_summary.py --json, committed as profiles/pmc_config<k>.json): HBM
+    bytes (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md), VALU instructions and GRBM cycles.  None when absent or
+    when this run is not the default configuration the passes were taken on."""
+    path = os.path.join(HERE, "profiles", f"pmc_config{args.config}.json")
+    if not default_config(args) or not os.path.exists(path):
         return None
     try:
         with open(path) as f:
-            return round(float(json.load(f)["traffic_bytes_per_launch"]), 1)
-    except (OSError, ValueError, KeyError):
+            return json.load(f)
+    except (OSError, ValueError):
         return None
 
 
-def cpu_baseline(desc, args):
-    """The CPU oracle (scalar C++ restatement, own SAH BVH) on a bounded sample
-    of the same frame: every k-th pixel, all spp, timed with steady_clock."""
+def gather_ceiling(bvh_nodes):
+    """Dependent random 64-B gather ceiling of this GPU (G fetches/s), measured now by
+    build/ubench_gather on a table of 2^floor(log2(bvh_nodes)) nodes (no larger
+    than the scene's node array, so the ceiling is not understated)."""
+    import subprocess
+
+    exe = os.path.join(HERE, "build", "ubench_gather")
+    if not os.path.exists(exe):
+        return None
+    log2 = max(12, int(np.floor(np.log2(max(2, bvh_nodes)))))
+    try:
+        r = subprocess.run([exe, str(log2), "--json"], capture_output=True, text=True, timeout=120)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError, subprocess.SubprocessError):
+        return None
+
+
+def roofline(args, st_bytes, trace_ms, trace_launches):
+    launches = max(1, st_bytes["trace_launches"])
+    ms = trace_ms / max(1, trace_launches)  # HIP events on the render stream, last timed frame
+    sec = ms * 1e-3
+    nodes = st_bytes["node_visits"] / launches
+    alg_bytes = st_bytes["trace_bytes"] / launches
+    kernel = ("k_trace4 (persistent BVH4 traversal, all launches of a frame: primary extend + "
+              "per-bounce extension+shadow)")
+    cands = {}
+    ceil = gather_ceiling(int(st_bytes["bvh_nodes"]))
+    if ceil and sec > 0:
+        cands["node-gather"] = {"achieved": nodes / sec / 1e9, "peak": ceil["ceiling_gnodes_per_s"],
+                                "unit": "Gnode/s",
+                                "how": "node visits per launch (instrumented frame) / HIP-event launch time; peak = "
+                                       f"build/ubench_gather dependent 64-B gathers, {ceil['table_mb']:.0f} MB table, "
+                                       "best waves/SIMD, measured in this run",
+                                "ceiling_per_waves_per_simd": ceil.get("per_waves_per_simd")}
+    pmc = pmc_record(args)
+    traffic = None
+    if pmc and sec > 0:
+        traffic = pmc["traffic_bytes_per_launch"]
+        cands["hbm"] = {"achieved": traffic / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "how": "PMC 2 x FETCH_SIZE + WRITE_SIZE per launch (profiles/pmc_config%d.json, %s) / "
+                               "HIP-event launch time" % (args.config, pmc.get("round", "?"))}
+        if pmc.get("valu_insts_per_launch") and pmc.get("clock_ghz"):
+            simds = 1024  # 256 CUs x 4 SIMD
+            # wave64 VALU op = 2 issue cycles on a SIMD-32 (MI355X_MICROARCH.md)
+            need = 2.0 * pmc["valu_insts_per_launch"]
+            have = simds * pmc["clock_ghz"] * 1e9 * sec
+            cands["valu-issue"] = {"achieved": need / sec / 1e9, "peak": simds * pmc["clock_ghz"], "unit": "G SIMD-cycles/s",
+                                   "how": "PMC SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) per launch over 1024 SIMDs at "
+                                          "the GRBM-measured clock"}
+    for c in cands.values():
+        c["frac"] = round(c["achieved"] / c["peak"], 4)
+        c["achieved"] = round(c["achieved"], 2)
+    out = {"kernel": kernel, "ms_per_launch": round(ms, 4), "traffic": round(traffic, 1) if traffic else None,
+           # SURVEY.md §8(d) algorithmic bytes (32 B ray + 16 B hit + 64 B/node + 48 B/primitive): the BVH
+           # is cache-resident (L2 + Infinity Cache), so these exceed what HBM delivers; not a fraction of HBM
+           "algorithmic": {"bytes_per_launch": round(alg_bytes, 1),
+                           "gbs": round(alg_bytes / sec / 1e9, 1) if sec > 0 else None},
+           "ceilings": cands}
+    if cands:
+        bound = max(cands, key=lambda k: cands[k]["frac"])
+        b = cands[bound]
+        out.update({"bound": bound, "achieved": b["achieved"], "peak": round(b["peak"], 2), "unit": b["unit"],
+                    "frac": b["frac"]})
+    else:
+        out.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None})
+    keys = ["bound", "achieved", "peak", "unit", "frac", "traffic"]
+    return {**{k: out[k] for k in keys}, **{k: v for k, v in out.items() if k not in keys}}
+
+
+def usable_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max":
+                n = min(n, max(1, int(np.ceil(int(quota) / int(period)))))
+        except (OSError, ValueError):
+            pass
+    return n
+
+
+def native_oracle():
+    """Build the oracle for THIS host (-O3 -march=native, same -ffp-contract=off, no
+    fast-math) into a scratch directory; None when no compiler is available."""
+    import subprocess
+    import tempfile
+
+    src = os.path.join(HERE, "oracle", "pt_oracle.cpp")
+    out = os.path.join(tempfile.gettempdir(), f"pupil_oracle_native_{os.getuid()}", "liboracle.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-march=native", "-ffp-contract=off", "-fno-fast-math", "-pthread",
+           "-shared", "-I", os.path.join(HERE, "include"), "-o", out, src]
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, timeout=300)
+        return out
+    except (OSError, subprocess.SubprocessError):
+        return None
+
+
+def cpu_baseline(desc, args, pt):
+    """The CPU oracle (scalar C++ restatement of the same integrator, its own
+    binned-SAH BVH2) on a bounded sample of the same frame: every k-th pixel, all
+    spp, on every usable host CPU, timed with steady_clock.  The sampled pixels
+    are also compared with the GPU frame just rendered (bit-exact expected)."""
+    native = native_oracle()
+    if native:
+        os.environ["PUPIL_ORACLE_LIB"] = native
     try:
         import oracle
     except Exception as e:  # pragma: no cover
         return {"error": str(e)}
     import platform
 
+    threads = args.cpu_threads or usable_cpus()
     osc = oracle.OracleScene(desc)
     npix = args.width * args.height
     pixels = np.arange(0, npix, args.cpu_sample_stride, dtype=np.uint32)
-    r = osc.render(spp=args.spp, max_depth=args.max_depth, pixels=pixels, threads=args.cpu_threads)
+    r = osc.render(spp=args.spp, max_depth=args.max_depth, pixels=pixels, threads=threads)
     s = r["stats"]
     rays = s["primary_rays"] + s["extension_rays"] + s["shadow_rays"]
+    gpu = pt.buffers.get("pt accum buffer").cpu().numpy().reshape(npix, 4)[pixels]
+    exact = int(np.all(gpu.view(np.uint32) == r["accum"].view(np.uint32), axis=1).sum())
     cpu_model = platform.processor()
     try:
         with open("/proc/cpuinfo") as f:
@@ -292,7 +398,10 @@ def cpu_baseline(desc, args):
             "kind": "port",
             "sample": f"every {args.cpu_sample_stride}th pixel ({len(pixels)} px) x {args.spp} spp of the same frame, "
                       f"{rays} rays in {s['seconds']:.2f}s",
-            "cpu": cpu_model}
+            "cpu": cpu_model, "host_cpus": os.cpu_count(), "usable_cpus": usable_cpus(),
+            "build": "g++ -O3 -march=native (built on this host)" if native else "prebuilt -march=x86-64-v2",
+            "bvh": "the oracle's own binned-SAH BVH2 (not the engine's BVH4; hits are BVH-independent)",
+            "gpu_pixels_bit_exact": f"{exact}/{len(pixels)}"}
 
 
 if __name__ == "__main__":

@@ -224,6 +224,16 @@ typedef struct pupil_pt_counters {
     double extend_bytes;
     double shade_ms;         /* device time of the shade stages (all materials) */
     uint64_t two_level;      /* 1: TLAS over instances + per-shape BLAS; 0: one flattened BVH */
+    /* collect_stats: loop iterations that reached the shadow test (main.cu:113-123),
+     * i.e. the shadow rays the reference traces unconditionally.  shadow_rays counts
+     * only the traced ones: the engine (and the oracle) test occlusion only when
+     * f * pdf_L != 0 and NoL > 0, which cannot change the radiance because
+     * Eval draws no random numbers (optix_material.h:57-62). */
+    uint64_t shadow_rays_reference;
+    /* BVH4 levels of the acceleration structure (two-level: TLAS + deepest BLAS); at
+     * create, trees needing more than the traversal stacks hold are rebuilt with the
+     * Karras LBVH or rejected with PUPIL_ERR_UNSUPPORTED */
+    uint64_t bvh_depth;
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;

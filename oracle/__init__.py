@@ -18,12 +18,14 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+# PUPIL_ORACLE_LIB: another build of the same source (bench.py's cpu_baseline builds
+# one with -march=native on the host it runs on)
+LIB_PATH = os.environ.get("PUPIL_ORACLE_LIB") or os.path.join(HERE, "_build", "liboracle.so")
 
 
 class OracleStats(C.Structure):
     _fields_ = [("primary_rays", C.c_uint64), ("extension_rays", C.c_uint64), ("shadow_rays", C.c_uint64),
-                ("seconds", C.c_double), ("threads", C.c_uint32)]
+                ("seconds", C.c_double), ("threads", C.c_uint32), ("shadow_rays_reference", C.c_uint64)]
 
 
 _LIB = None

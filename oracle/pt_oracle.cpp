@@ -1426,7 +1426,7 @@ struct FrameOut {
 
 void RenderPixel(const Scene &sc, unsigned int pixel_index, unsigned int out_index, unsigned int random_seed,
                  unsigned int sample_cnt, bool accumulated_flag, unsigned int max_depth, bool write_aov,
-                 const FrameOut &out, uint64_t counts[3]) {
+                 const FrameOut &out, uint64_t counts[4]) {
     const unsigned int w = sc.width, h = sc.height;
     const unsigned int ix = pixel_index % w, iy = pixel_index / w;
     float3 radiance = make_float3(0.f), env_radiance = make_float3(0.f), throughput = make_float3(1.f);
@@ -1497,6 +1497,7 @@ void RenderPixel(const Scene &sc, unsigned int pixel_index, unsigned int out_ind
         float rr = depth > 2 ? 0.95 : 1.0;
         if (random.Next() > rr) break;
         throughput /= rr;
+        counts[3]++;  // the reference traces its shadow ray here unconditionally (main.cu:119-123)
         {
             const Emitter *emitter = sc.emitters.SelectOneEmiiter(random.Next());
             EmitterSampleRecord esr;
@@ -1510,7 +1511,12 @@ void RenderPixel(const Scene &sc, unsigned int pixel_index, unsigned int out_ind
                 bsdf.Eval(eval_record);
                 const float3 f = eval_record.f;
                 const float pdf = eval_record.pdf;
-                // the occlusion test only matters when the contribution is non-zero
+                // Reordered from main.cu:119-141, radiance-equivalent: the reference traces the
+                // shadow ray first and calls Eval only when unoccluded, but Eval (GetBsdf +
+                // GetPdf) draws no random numbers (optix_material.h:57-62; only Sample does,
+                // bsdf/*.h), so testing occlusion only for a non-zero contribution changes no
+                // pixel and no later RNG draw.  counts[2] = shadow rays traced here, counts[3] =
+                // the reference's unconditional count.
                 if (!IsZero(f * esr.pdf)) {
                     const float NoL = dot(geo.normal, esr.wi);
                     if (NoL > 0.f) {
@@ -1574,6 +1580,7 @@ struct oracle_stats {
     uint64_t primary_rays, extension_rays, shadow_rays;
     double seconds;
     uint32_t threads;
+    uint64_t shadow_rays_reference;  // loop iterations reaching main.cu:119-123
 };
 
 typedef struct oracle_scene oracle_scene;
@@ -1604,10 +1611,10 @@ int oracle_render(oracle_scene *s, uint32_t random_seed, uint32_t sample_cnt, ui
     }
     oracle::FrameOut out{accum, albedo, normal, test};
     std::atomic<uint32_t> next{0};
-    std::atomic<uint64_t> c0{0}, c1{0}, c2{0};
+    std::atomic<uint64_t> c0{0}, c1{0}, c2{0}, c3{0};
     const auto t0 = std::chrono::steady_clock::now();
     auto worker = [&]() {
-        uint64_t counts[3] = {0, 0, 0};
+        uint64_t counts[4] = {0, 0, 0, 0};
         const uint32_t chunk = 64;
         while (true) {
             const uint32_t b = next.fetch_add(chunk);
@@ -1622,6 +1629,7 @@ int oracle_render(oracle_scene *s, uint32_t random_seed, uint32_t sample_cnt, ui
         c0 += counts[0];
         c1 += counts[1];
         c2 += counts[2];
+        c3 += counts[3];
     };
     std::vector<std::thread> pool;
     for (int t = 0; t < threads; t++) pool.emplace_back(worker);
@@ -1633,6 +1641,7 @@ int oracle_render(oracle_scene *s, uint32_t random_seed, uint32_t sample_cnt, ui
         stats->shadow_rays = c2;
         stats->seconds = std::chrono::duration<double>(t1 - t0).count();
         stats->threads = (uint32_t)threads;
+        stats->shadow_rays_reference = c3;
     }
     return 0;
 }

@@ -86,7 +86,8 @@ class Counters(C.Structure):
                 ("trace_ms", C.c_double), ("trace_bytes", C.c_double), ("trace_launches", C.c_uint64),
                 ("extend_ms", C.c_double), ("extend_launches", C.c_uint64), ("extend_node_visits", C.c_uint64),
                 ("extend_prim_tests", C.c_uint64), ("extend_bytes", C.c_double), ("shade_ms", C.c_double),
-                ("two_level", C.c_uint64)]
+                ("two_level", C.c_uint64), ("shadow_rays_reference", C.c_uint64),
+                ("bvh_depth", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

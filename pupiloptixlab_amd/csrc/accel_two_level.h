@@ -22,6 +22,7 @@ struct TwoLevelAccel {
     float *d_boxes = nullptr;    // 6 floats per instance: world box
     uint32_t *d_list = nullptr, *d_verts = nullptr;  // scratch: instance list, vertices per instance
     uint32_t tlas_cap = 0, tlas_nodes = 0, num_nodes4 = 0, num_prims = 0;
+    uint32_t tlas_depth = 0, blas_depth = 0;  // BVH4 levels (deepest BLAS); see kTraceStackEntries
     uint32_t root_link4 = (uint32_t)kTraverseDone;
     double build_ms = 0.0;
 };
@@ -40,7 +41,8 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
                     std::vector<DevInstance> &insts, DevInstance *d_insts, const DevMaterial *d_mats,
                     uint32_t leaf_size, hipStream_t s, TwoLevelAccel &acc);
 // Recomputes the world boxes of the `changed` instances (transforms already in
-// insts / d_insts) and rebuilds the TLAS.
+// insts / d_insts) and rebuilds the TLAS.  -3: the TLAS + BLAS depth exceeds the
+// traversal stacks (kTraceStackEntries).
 int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstance *d_insts,
                  const std::vector<uint32_t> &changed, hipStream_t s);
 void free_two_level(TwoLevelAccel &acc);

@@ -155,8 +155,9 @@ uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std
 
 // 4-wide TLAS node over ids[b, e) (two levels of binary SAH splits); returns its link.
 int build_tlas_node(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std::vector<HostBox> &boxes,
-                    std::vector<Bvh4Node> &nodes) {
+                    std::vector<Bvh4Node> &nodes, uint32_t level, uint32_t &depth) {
     if (e - b == 1) return make_leaf(ids[b], 1u);
+    depth = std::max(depth, level + 1);
     uint32_t ranges[4][2];
     int nk = 0;
     const uint32_t m = sah_split(ids, b, e, boxes);
@@ -186,7 +187,7 @@ int build_tlas_node(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const st
             clo[a][k] = cb.lo[a];
             chi[a][k] = cb.hi[a];
         }
-        link[k] = build_tlas_node(ids, ranges[k][0], ranges[k][1], boxes, nodes);
+        link[k] = build_tlas_node(ids, ranges[k][0], ranges[k][1], boxes, nodes, level + 1, depth);
     }
     nodes[self] = encode_bvh4(nb.lo, nb.hi, clo, chi, link, nk);
     return (int)self;
@@ -248,8 +249,13 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
     for (uint32_t i = 0; i < n; i++)
         if (insts[i].kind == PUPIL_SHAPE_SPHERE || insts[i].blas_root != kTraverseDone) ids.push_back(i);
     std::vector<Bvh4Node> nodes;
-    const int root = ids.empty() ? kTraverseDone : build_tlas_node(ids, 0, (uint32_t)ids.size(), boxes, nodes);
+    uint32_t depth = 0;
+    const int root =
+        ids.empty() ? kTraverseDone : build_tlas_node(ids, 0, (uint32_t)ids.size(), boxes, nodes, 0u, depth);
     if (nodes.size() > acc.tlas_cap) return -1;
+    // a lane inside a BLAS holds the TLAS entries, the pending link + kReturnLink and the BLAS entries
+    if (3u * depth + 2u + 3u * acc.blas_depth > (uint32_t)kTraceStackEntries) return -3;
+    acc.tlas_depth = depth;
     if (!nodes.empty() &&
         hipMemcpyAsync(acc.nodes4, nodes.data(), sizeof(Bvh4Node) * nodes.size(), hipMemcpyHostToDevice, s) !=
             hipSuccess)
@@ -304,9 +310,13 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         }
         BvhBuildInput bin{sh.num_faces, zeros, d_ident, d_mats, 1u};
         double ms = 0.0;
-        if (sh.num_faces && build_lbvh(bin, blas[k], leaf_size, s, &ms) != 0) {
-            rc = -1;
-            break;
+        if (sh.num_faces) {
+            const int brc = build_bvh_bounded(bin, blas[k], leaf_size, s, &ms, 2u);
+            if (brc != 0) {
+                rc = brc == -3 ? -3 : -1;
+                break;
+            }
+            acc.blas_depth = std::max(acc.blas_depth, blas[k].depth4);
         }
         node_base[k] = total_nodes;
         prim_base[k] = total_prims;
@@ -367,11 +377,12 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         verts[i] = shapes[k].num_vertices;
         instance_margin(d, shapes[k].vmax);
     }
+    int trc = 0;
     if (hipMemcpy(acc.d_verts, verts.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_insts, insts.data(), sizeof(DevInstance) * n, hipMemcpyHostToDevice) != hipSuccess ||
-        rebuild_tlas(acc, insts, d_insts, all, s) != 0) {
+        (trc = rebuild_tlas(acc, insts, d_insts, all, s)) != 0) {
         free_two_level(acc);
-        return -1;
+        return trc == -3 ? -3 : -1;
     }
     acc.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return 0;

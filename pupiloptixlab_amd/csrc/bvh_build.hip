@@ -767,7 +767,7 @@ hipError_t dmalloc(T **p, size_t count) {
 // nodes4 must hold n - 1 entries; returns the number of 4-wide nodes.
 hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
                          const int2 *ranges, const Aabb *node_boxes, uint32_t leaf_size, Bvh4Node *nodes4,
-                         uint32_t *num_nodes4, hipStream_t s) {
+                         uint32_t *num_nodes4, uint32_t *depth4, hipStream_t s) {
     int *items_a = nullptr, *items_b = nullptr;
     int4 *clist = nullptr;
     unsigned long long *cnt = nullptr, *sums = nullptr, *total = nullptr;
@@ -780,6 +780,7 @@ hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_bo
     if (!err) err = dmalloc(&sums, (cap + per - 1) / per);
     if (!err) err = dmalloc(&total, 1);
     int base = 0, items = 1;
+    uint32_t levels = 0;  // breadth first: one iteration per BVH4 level
     if (!err) err = hipMemsetAsync(items_a, 0, sizeof(int), s);  // binary root 0
     const auto grid = [](int m) { return dim3((unsigned)((m + kBlock - 1) / kBlock)); };
     while (!err && items > 0) {
@@ -796,10 +797,12 @@ hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_bo
         err = hipStreamSynchronize(s);
         base += items;
         items = (int)tot;
+        levels++;
         if (base + items > n - 1) err = hipErrorUnknown;  // cannot happen
         std::swap(items_a, items_b);
     }
     *num_nodes4 = (uint32_t)base;
+    *depth4 = levels;
     void *bufs[] = {items_a, items_b, clist, cnt, sums, total};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -890,7 +893,8 @@ void free_lbvh(BvhBuildOutput &out) {
     out.attrs = nullptr;
 }
 
-int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms) {
+int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms,
+               bool force_lbvh) {
     const int n = (int)in.num_prims;
     if (n <= 0) {  // empty scene: every ray misses
         out = BvhBuildOutput{};
@@ -900,6 +904,7 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     }
     if (leaf_size < 1) leaf_size = 1;
     if (leaf_size > (uint32_t)kLeafMax) leaf_size = kLeafMax;
+    out.depth4 = 0;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
@@ -954,7 +959,7 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
             (void)hipMemsetAsync(flags, 0, sizeof(uint32_t) * n, s);
             const uint32_t gi = (uint32_t)((n - 1 + kBlock - 1) / kBlock);
             const char *builder = std::getenv("PUPIL_BVH_BUILDER");
-            const bool ploc = !(builder && std::strcmp(builder, "lbvh") == 0);
+            const bool ploc = !force_lbvh && !(builder && std::strcmp(builder, "lbvh") == 0);
             if (ploc) {
                 err = build_ploc(n, vi, vo, boxes, children, ranges, node_boxes, parent_internal, parent_leaf, s);
                 uint32_t *t = vi;  // vo holds the PLOC primitive order
@@ -974,7 +979,7 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
                 err = dmalloc(&out.nodes4, (size_t)(n - 1));
                 if (!err)
                     err = collapse_bvh4(n, vi, boxes, children, ranges, node_boxes, leaf_size, out.nodes4,
-                                        &out.num_nodes4, s);
+                                        &out.num_nodes4, &out.depth4, s);
             } else if (!err) {
             // 4-wide quantized tree: depth parity -> flags -> compact indices -> nodes
             uint32_t *depth = ko, *flags4 = vo, *idx4 = nullptr;  // the sort's free ping-pong buffers
@@ -1004,6 +1009,7 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
         hipLaunchKernelGGL(k_reorder, dim3(g), dim3(kBlock), 0, s, n, vi, recs, out.prims);
         hipLaunchKernelGGL(k_attrs, dim3(g), dim3(kBlock), 0, s, n, vi, in, out.attrs);
         out.num_nodes = n > 1 ? (uint32_t)(n - 1) : 0u;
+        if (n == 1 || (uint32_t)n <= leaf_size) out.depth4 = 1;  // the root is a leaf
         out.root_link = ((uint32_t)n <= leaf_size) ? (uint32_t)make_leaf(0u, (uint32_t)n) : 0u;
         out.root_link4 = out.root_link;
         if (!err) err = hipGetLastError();
@@ -1030,6 +1036,27 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     (void)hipFree(parent_internal);
     (void)hipFree(parent_leaf);
     return err == hipSuccess ? 0 : -2;
+}
+
+int build_bvh_bounded(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s,
+                      double *build_ms, uint32_t reserve) {
+    const auto fits = [&](const BvhBuildOutput &o) {
+        return o.depth4 == 0 || 3u * o.depth4 + reserve <= (uint32_t)kTraceStackEntries;
+    };
+    int rc = build_lbvh(in, out, leaf_size, s, build_ms);
+    if (rc != 0 || fits(out)) return rc;
+    // PLOC merges nearest neighbours bottom-up and can chain a skewed primitive
+    // distribution into a deep tree; the Karras LBVH splits on Morton bits.
+    free_lbvh(out);
+    double ms2 = 0.0;
+    rc = build_lbvh(in, out, leaf_size, s, &ms2, true);
+    if (build_ms) *build_ms += ms2;
+    if (rc != 0) return rc;
+    if (!fits(out)) {
+        free_lbvh(out);
+        return -3;
+    }
+    return 0;
 }
 
 }  // namespace pupil

@@ -339,7 +339,7 @@ uint32_t local_pixels(uint32_t w, uint32_t h, uint32_t ts, uint32_t rank, uint32
 extern "C" {
 
 const char *pupil_last_error(void) { return g_last_error.c_str(); }
-int pupil_abi_version(void) { return 1; }
+int pupil_abi_version(void) { return 2; }
 
 int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank, uint32_t tile_world,
                           uint32_t *out_pixels, uint32_t *inout_count) {
@@ -511,13 +511,15 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
                 for (size_t v = 0; v < 3 * (size_t)sh.num_vertices; v++) vmax = std::max(vmax, std::fabs(sh.positions[v]));
                 t.vmax = vmax;
             }
-            if (build_two_level(tls, inst_shape, insts, d_insts, d_mats, pt->leaf_size, pt->own_stream, pt->tl) != 0)
-                return cleanup(fail(PUPIL_ERR_HIP, "two-level acceleration build failed"));
+            const int trc = build_two_level(tls, inst_shape, insts, d_insts, d_mats, pt->leaf_size, pt->own_stream, pt->tl);
+            if (trc == -3) return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "TLAS + BLAS deeper than the traversal stacks hold"));
+            if (trc != 0) return cleanup(fail(PUPIL_ERR_HIP, "two-level acceleration build failed"));
             pt->build_ms = pt->tl.build_ms;
         } else {
             BvhBuildInput bin{pt->num_prims, d_prim_inst, d_insts, d_mats};
-            if (build_lbvh(bin, pt->bvh, pt->leaf_size, pt->own_stream, &pt->build_ms) != 0)
-                return cleanup(fail(PUPIL_ERR_HIP, "LBVH build failed"));
+            const int brc = build_bvh_bounded(bin, pt->bvh, pt->leaf_size, pt->own_stream, &pt->build_ms, 0);
+            if (brc == -3) return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "BVH deeper than the traversal stacks hold"));
+            if (brc != 0) return cleanup(fail(PUPIL_ERR_HIP, "LBVH build failed"));
         }
     }
     pt->h_insts = insts;
@@ -559,7 +561,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     std::memcpy(sc.camera.c2w, scene->camera_to_world, sizeof(sc.camera.c2w));
     // traversal overflow stacks, counters, events
     pt->ovf_threads = trace_grid_blocks() * (uint32_t)kTraceBlock;
-    if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 16) ||
+    if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 32) ||
         pt->alloc(&pt->ray_log, 2 * 130) || pt->alloc(&pt->q.counts, kCountSlots) ||
         pt->alloc(&pt->q.work, kWorkSlots))
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
@@ -570,6 +572,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     pt->totals.bvh_nodes = pt->two_level ? pt->tl.tlas_nodes + (pt->tl.num_nodes4 - pt->tl.tlas_cap)
                            : (pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes);
     pt->totals.two_level = pt->two_level ? 1u : 0u;
+    pt->totals.bvh_depth = pt->two_level ? pt->tl.tlas_depth + pt->tl.blas_depth : pt->bvh.depth4;
     pt->totals.bvh_prims = pt->num_prims;
     pt->totals.build_ms = pt->build_ms;
     *out = pt;
@@ -598,19 +601,23 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     HIP_TRY(hipMemcpy(pt->d_insts + instance, &d, sizeof(DevInstance), hipMemcpyHostToDevice));
     if (pt->two_level) {  // new world box for the instance, TLAS rebuilt over all instance boxes
         const auto t0 = std::chrono::steady_clock::now();
-        if (rebuild_tlas(pt->tl, pt->h_insts, pt->d_insts, {instance}, pt->own_stream) != 0)
-            return fail(PUPIL_ERR_HIP, "TLAS rebuild failed");
+        const int trc = rebuild_tlas(pt->tl, pt->h_insts, pt->d_insts, {instance}, pt->own_stream);
+        if (trc == -3) return fail(PUPIL_ERR_UNSUPPORTED, "TLAS + BLAS deeper than the traversal stacks hold");
+        if (trc != 0) return fail(PUPIL_ERR_HIP, "TLAS rebuild failed");
         pt->sc.root_link4 = pt->tl.root_link4;
         pt->totals.bvh_nodes = pt->tl.tlas_nodes + (pt->tl.num_nodes4 - pt->tl.tlas_cap);
+        pt->totals.bvh_depth = pt->tl.tlas_depth + pt->tl.blas_depth;
         pt->totals.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         return PUPIL_OK;
     }
     BvhBuildInput bin{pt->num_prims, pt->d_prim_inst, pt->d_insts, pt->d_mats};
     BvhBuildOutput nb{};
     double ms = 0.0;
-    if (build_lbvh(bin, nb, pt->leaf_size, pt->own_stream, &ms) != 0) {
+    const int brc = build_bvh_bounded(bin, nb, pt->leaf_size, pt->own_stream, &ms, 0);
+    if (brc != 0) {
         free_lbvh(nb);
-        return fail(PUPIL_ERR_HIP, "LBVH rebuild failed");
+        return fail(brc == -3 ? PUPIL_ERR_UNSUPPORTED : PUPIL_ERR_HIP,
+                    brc == -3 ? "BVH deeper than the traversal stacks hold" : "LBVH rebuild failed");
     }
     free_lbvh(pt->bvh);
     pt->bvh = nb;
@@ -621,6 +628,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     pt->sc.nodes4 = nb.nodes4;
     pt->sc.root_link4 = nb.root_link4;
     pt->totals.bvh_nodes = pt->sc.bvh_width == 4 ? nb.num_nodes4 : nb.num_nodes;
+    pt->totals.bvh_depth = nb.depth4;
     pt->totals.build_ms = ms;
     return PUPIL_OK;
 }
@@ -638,6 +646,10 @@ int pupil_pt_update_emitters(pupil_pt *pt, const pupil_scene_desc *scene) {
 int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_launch *launch, void *hip_stream) {
     if (!pt || !out || !launch || !out->accum) return fail(PUPIL_ERR_INVALID, "null argument");
     if (launch->spp == 0) return PUPIL_OK;
+    // PTPass clamps the inspector's max_depth to 1..128 (pt_pass.cpp:225-237); the
+    // per-bounce ray log and the stage-event list are sized for that range
+    if ((launch->max_depth ? launch->max_depth : pt->max_depth) > kMaxDepth)
+        return fail(PUPIL_ERR_INVALID, "max_depth above 128");
     const uint32_t world = launch->tile_world ? launch->tile_world : 1u;
     const uint32_t ts = launch->tile_size ? launch->tile_size : 32u;
     if (launch->tile_rank >= world) return fail(PUPIL_ERR_INVALID, "tile_rank >= tile_world");
@@ -686,6 +698,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     fp.albedo = (float *)out->albedo;
     fp.normal = (float *)out->normal;
     fp.test = (float *)out->test;
+    fp.nee_count = launch->collect_stats ? pt->trace_counters + 16 : nullptr;
 
     const bool stats = launch->collect_stats != 0;
     TraceStats ts_dev{pt->trace_counters};
@@ -710,7 +723,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     };
 
     HIP_TRY(hipEventRecord(pt->ev_begin, s));
-    if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 16 * sizeof(unsigned long long), s));
+    if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 32 * sizeof(unsigned long long), s));
     const uint32_t np = fp.num_paths;
     Queues &q = pt->q;
     // material bins of the traced paths -> q.bins (stable, increasing path id)
@@ -796,7 +809,7 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
         c.extend_launches = kind_n[0];
         c.shade_ms = kind_ms[2];
         if (pt->last_stats) {
-            unsigned long long tc[16];
+            unsigned long long tc[32];
             HIP_TRY(hipMemcpy(tc, pt->trace_counters, sizeof(tc), hipMemcpyDeviceToHost));
             for (int k = 0; k < 2 && std::getenv("PUPIL_TRACE_DIAG"); k++) {  // SIMD efficiency, persistent kernels
                 const unsigned long long *d = tc + 2 + 6 * k;
@@ -810,6 +823,7 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
             }
             c.node_visits = tc[0] + tc[14];
             c.prim_tests = tc[1] + tc[15];
+            c.shadow_rays_reference = tc[16];
             c.extend_node_visits = tc[0];
             c.extend_prim_tests = tc[1];
             const double rays = (double)(c.primary_rays + c.extension_rays + c.shadow_rays);
@@ -829,6 +843,7 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
     if (!pt || !rays || !out) return fail(PUPIL_ERR_INVALID, "null argument");
     if (n == 0) return PUPIL_OK;
     HIP_TRY(hipSetDevice(pt->device));
+    HIP_TRY(hipDeviceSynchronize());  // no render on another stream may still use the shared overflow stacks
     float *d_rays = nullptr, *d_out = nullptr;
     HIP_TRY(hipMalloc((void **)&d_rays, sizeof(float) * 8 * (size_t)n));
     hipError_t e = hipMalloc((void **)&d_out, sizeof(float) * 4 * (size_t)n);

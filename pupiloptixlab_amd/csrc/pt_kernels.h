@@ -12,8 +12,15 @@ constexpr int kTraceBlock = 128;
 constexpr int kTraceWavesPerSimd = 7;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8: 2 % slower)
 constexpr int kTraceWavesPerSimdTL = 4;  // two-level variant (<= 128 VGPRs)
 constexpr int kStackLds = 32;   // per-thread LDS stack entries
-constexpr int kStackOvf = 96;   // per-thread global overflow entries
+constexpr int kStackOvf = 160;  // per-thread global overflow entries
+constexpr int kRing = 16;       // persistent BVH4 kernels: per-lane LDS ring entries (spills to the overflow column)
+// Stack entries a traversal may need: 3 per BVH4 level (4 children, one taken), plus
+// 2 per instance entry in two-level mode.  Builds whose trees need more are rejected
+// (or rebuilt with the depth-bounded Karras LBVH) at create time, so no kernel ever
+// overwrites a live entry.
+constexpr int kTraceStackEntries = kRing + kStackOvf < kStackLds + kStackOvf ? kRing + kStackOvf : kStackLds + kStackOvf;
 constexpr int kShadeBlock = 256;
+constexpr uint32_t kMaxDepth = 128;  // PTPass inspector range (pt_pass.cpp:225-237)
 constexpr uint32_t kNumQueues = 9;  // 0 = miss, 1..7 = EMatType, 8 = unknown material
 constexpr uint32_t kMissIndex = 0xFFFFFFFFu;
 
@@ -89,6 +96,7 @@ struct FrameParams {
     float *albedo;  // 3 floats per pixel
     float *normal;
     float *test;
+    unsigned long long *nee_count;  // collect_stats: paths that reached the shadow test (main.cu:113-123)
 };
 
 struct TraceStats {
@@ -136,8 +144,15 @@ struct BvhBuildOutput {
     uint32_t root_link4;
     uint32_t num_nodes;
     uint32_t num_nodes4;
+    uint32_t depth4;    // levels of the BVH4 (1 = root only); 0 = not measured (A/B collapse)
 };
-int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms);
+int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms,
+               bool force_lbvh = false);
+// build_lbvh whose BVH4 fits the traversal stacks with `reserve` entries to spare:
+// PLOC first, the Karras LBVH (depth bounded by the 30-bit Morton codes) when the
+// PLOC tree is too deep.  Returns 0, -2 on a HIP error, -3 when no tree fits.
+int build_bvh_bounded(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s,
+                      double *build_ms, uint32_t reserve);
 void free_lbvh(BvhBuildOutput &out);
 
 }  // namespace pupil

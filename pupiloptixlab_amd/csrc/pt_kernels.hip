@@ -427,7 +427,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow(DeviceScene sc, PathStat
 // (Aila & Laine 2009, "dynamic fetch"), so a wave never idles on its longest
 // ray.  The stack is a 16-entry LDS ring per lane that spills its oldest 8
 // entries to HBM when full, so push/pop are LDS-only in the common case.
-constexpr int kRing = 16;
 constexpr int kSpill = 8;
 static_assert((kRing & (kRing - 1)) == 0, "ring size must be a power of two");
 
@@ -440,10 +439,9 @@ struct RingStack {
 
     __device__ __forceinline__ int &slot(int i) { return lds[(i & (kRing - 1)) * kTraceBlock]; }
     __device__ __forceinline__ void reset() { sp = bot = 0; }
-    // Make room for three pushes.  When the overflow column is exhausted too
-    // (stack deeper than kRing + kStackOvf, impossible for trees of depth
-    // <= 32) the oldest entries are overwritten: a wrong answer, never an
-    // out-of-bounds access.
+    // Make room for three pushes.  The overflow column holds kStackOvf entries;
+    // create() rejects trees needing more than kTraceStackEntries (3 per BVH4
+    // level + 2 per instance entry), so the guard below never triggers.
     __device__ __forceinline__ void reserve3() {
         if (sp + 3 - bot > kRing && bot + kSpill <= kStackOvf) {
 #pragma unroll
@@ -1099,6 +1097,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     }
     float pdf_b = 0.f;
     uint32_t delta = 0;
+    const bool nee = alive;  // the reference traces its shadow ray here unconditionally (main.cu:119-123)
     if (alive) {
         // direct light sampling (main.cu:114-141)
         float sel_prob;
@@ -1151,7 +1150,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     ps.rad[p] = f4(L, 0.f);
     ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 8), __float_as_uint(geo.texcoord.x),
                             __float_as_uint(geo.texcoord.y));
-    return (push_next ? 1u : 0u) | (push_shadow ? 2u : 0u);
+    return (push_next ? 1u : 0u) | (push_shadow ? 2u : 0u) | (nee ? 4u : 0u);
 }
 
 // Paths whose ray left the scene (__miss__default, main.cu:196-212, and the
@@ -1222,7 +1221,12 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, Frame
         case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p, bounce); break;
         default: flags = shade_hit<0u>(sc, fp, ps, p, bounce); break;
         }
-        ps.sflags[p] = (uint8_t)(flags | tag << 2);
+        if (fp.nee_count) {  // collect_stats only: the reference's shadow-ray count, one atomic per wave
+            const unsigned long long m = __ballot((flags & 4u) != 0u);
+            if (m && __lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_read_exec()) - 1)
+                atomicAdd(fp.nee_count, (unsigned long long)__popcll(m));
+        }
+        ps.sflags[p] = (uint8_t)((flags & 3u) | tag << 2);
         ps.mbin[p] = 0xFFu;  // listed again only if the next extend traces this path
     }
 }
@@ -1250,12 +1254,13 @@ __global__ __launch_bounds__(kShadeBlock) void k_accumulate(FrameParams fp, Path
 __global__ __launch_bounds__(kTraceBlock) void k_trace_debug(DeviceScene sc, const float *rays, float *out,
                                                              uint32_t n, int any, int *ovf, uint32_t ovf_threads) {
     __shared__ int s_stack[kStackLds * kTraceBlock];
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    // grid-stride over at most ovf_threads threads: thread g owns overflow column g
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     Stack st;
     st.lds = s_stack + threadIdx.x;
-    st.ovf = ovf + (i % ovf_threads);
+    st.ovf = ovf + g;
     st.ovf_stride = ovf_threads;
+    for (uint32_t i = g; i < n; i += gridDim.x * blockDim.x) {
     const float *r8 = rays + 8 * (size_t)i;
     const RayPre r = ray_pre(v3(r8[0], r8[1], r8[2]), v3(r8[3], r8[4], r8[5]));
     float tmax = r8[7];
@@ -1274,6 +1279,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_debug(DeviceScene sc, con
     o[1] = b1;
     o[2] = b2;
     o[3] = __uint_as_float(hit && !any ? key : 0xFFFFFFFFu);
+    }
 }
 
 __global__ void k_debug_math(const float *x, const float *y2, float *out, uint32_t n) {
@@ -1348,8 +1354,8 @@ void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, ui
                                PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
         return;
     }
-    hipLaunchKernelGGL(k_trace_debug, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, s, sc, rays,
-                       out, n, any, ovf, ovf_threads);
+    const uint32_t blocks = std::min((n + kTraceBlock - 1) / kTraceBlock, std::max(1u, ovf_threads / kTraceBlock));
+    hipLaunchKernelGGL(k_trace_debug, dim3(blocks), dim3(kTraceBlock), 0, s, sc, rays, out, n, any, ovf, ovf_threads);
 }
 
 void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, hipStream_t s) {

@@ -63,15 +63,19 @@ class FrameGather:
         A side stream waits for `stream`'s work so far, snapshots `local` into the
         send buffer, runs the collective and (rank 0) the scatter into the full
         image; `stream` waits only for the snapshot, so the next frame may start
-        at once and overwrite `local`.  The full image is valid once the side
-        stream has drained (wait() or torch.cuda.synchronize()).  Side-stream work
-        of consecutive calls runs in call order, so the send/recv buffers are
-        reused safely.  CPU tensors (gloo) take the synchronous path."""
+        at once and overwrite `local`.  Returns a GatherHandle: the full image is
+        not usable until ``handle.wait(stream)`` (device-side: `stream` waits for
+        the scatter) or ``handle.synchronize()`` (host).  Side-stream work of
+        consecutive calls runs in call order, and each call's side work first
+        waits for everything enqueued on `stream` before it, so a consumer that
+        waited on the handle and then read the image on `stream` is never
+        overwritten by a later frame.  CPU tensors / gloo take the synchronous
+        path and return an already-complete handle."""
         import torch
         import torch.distributed as dist
 
         if local.device.type != "cuda":
-            return self.gather(local)
+            return GatherHandle(self.gather(local), None)
         if dist.get_backend() != "nccl":  # rehearsal over gloo: stage through host memory, synchronously
             host = FrameGather.__new__(FrameGather)
             host.__dict__.update(self.__dict__)
@@ -81,14 +85,15 @@ class FrameGather:
             full = host.gather(local.cpu())
             if self.rank == 0:
                 self.full.copy_(full)
-                return self.full
-            return None
+                return GatherHandle(self.full, None)
+            return GatherHandle(None, None)
         if self._side is None:
             self._side = torch.cuda.Stream(device=local.device)
             self._copied = torch.cuda.Event()
         stream = stream if stream is not None else torch.cuda.current_stream(local.device)
         ready = torch.cuda.Event()
         ready.record(stream)
+        done = torch.cuda.Event()
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
             self.send[: self.n_local].copy_(local)
@@ -97,10 +102,36 @@ class FrameGather:
             if self.rank == 0:
                 for r in range(self.world):
                     self.full.index_copy_(0, self.maps[r], self.recv[r][: self.counts[r]])
+            done.record(self._side)
         stream.wait_event(self._copied)
-        return self.full if self.rank == 0 else None
+        return GatherHandle(self.full if self.rank == 0 else None, done)
 
     def wait(self):
         """Block the host until every gather_async() so far has completed."""
         if self._side is not None:
             self._side.synchronize()
+
+
+class GatherHandle:
+    """Completion of one FrameGather.gather_async(): the rank-0 image is valid on a
+    stream after wait(stream), on the host after synchronize()."""
+
+    def __init__(self, full, event):
+        self._full, self._event = full, event
+
+    def wait(self, stream=None):
+        """Make `stream` (default: the current stream) wait for the scatter; returns
+        the full image (rank 0) or None."""
+        if self._event is not None:
+            import torch
+
+            (stream if stream is not None else torch.cuda.current_stream()).wait_event(self._event)
+        return self._full
+
+    def synchronize(self):
+        if self._event is not None:
+            self._event.synchronize()
+        return self._full
+
+    def done(self) -> bool:
+        return self._event is None or self._event.query()

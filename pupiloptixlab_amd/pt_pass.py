@@ -101,6 +101,7 @@ class PTPass(Pass):
         self.sample_cnt = 0
         self.dirty = True
         self.tile = (32, 0, 1)  # tile_size, rank, world
+        self._world = None  # the World the scene came from: its sensor is re-read when dirty
         self.events = events or Events()
         self.events.bind(Events.CAMERA_CHANGE, lambda _: self.mark_dirty())
         self.events.bind(Events.RENDER_INSTANCE_UPDATE, self._on_instance_update)
@@ -172,6 +173,7 @@ class PTPass(Pass):
     # ---- PTPass::SetScene (pt_pass.cpp:107-209)
     def set_scene(self, world):
         desc = world.desc() if hasattr(world, "desc") else world
+        self._world = world if hasattr(world, "desc") else None
         self.close_engine()
         self._torch.cuda.set_device(self.device_index)
         check(self._lib.pupil_pt_create(C.byref(desc), self.device_index, C.byref(self._pt)))
@@ -206,7 +208,10 @@ class PTPass(Pass):
 
     def render(self, spp: int = 1, collect_stats: bool = False, stream=None):
         """spp consecutive OnRun frames in one wavefront batch (asynchronous)."""
-        if self.dirty:  # pt_pass.cpp:40-49
+        if self.dirty:  # pt_pass.cpp:40-49: camera re-uploaded, accumulation restarted
+            if self._world is not None:
+                d = self._world.desc()
+                check(self._lib.pupil_pt_set_camera(self._pt, d.sample_to_camera, d.camera_to_world))
             self.random_seed = 0
             self.sample_cnt = 0
             self.dirty = False

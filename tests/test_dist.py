@@ -31,7 +31,9 @@ def _worker(rank, world, port, w, h, tile, out_path):
     pix = local_pixels(w, h, tile, rank, world)
     local = torch.from_numpy(np.stack([pix, pix * 2, pix * 3, np.ones_like(pix)], 1).astype(np.float32))
     full = g.gather(local)
-    again = g.gather_async(local)  # CPU tensors: the synchronous path, same result
+    h = g.gather_async(local)  # CPU tensors: the synchronous path, same result
+    assert h.done()
+    again = h.synchronize()
     if rank == 0:
         assert torch.equal(full, again)
         np.save(out_path, full.numpy())
@@ -79,9 +81,12 @@ def test_gather_async_on_gpu_single_rank():
         s = torch.cuda.current_stream(dev)
         pix = torch.arange(w * h, dtype=torch.float32, device=dev)
         local = torch.stack([pix, 2 * pix, 3 * pix, torch.ones_like(pix)], 1)
-        full = g.gather_async(local, s)
+        h = g.gather_async(local, s)
         local.fill_(-1.0)  # the next frame overwrites the tile buffer on the render stream
+        full = h.wait(s)  # the render stream waits for the scatter before reading the image
+        full = full.clone()
         torch.cuda.synchronize(dev)
+        assert h.done()
         assert torch.equal(full[:, 1], 2 * pix)
         assert torch.equal(full[:, 3], torch.ones_like(pix))
     finally:

@@ -40,7 +40,7 @@ def render_gpu(desc, spp, seed=0, cnt=0, max_depth=0, accumulate=True, tile=(32,
     pt.random_seed, pt.sample_cnt = seed, cnt
     if prev is not None:
         pt.buffers.get("pt accum buffer").copy_(torch.from_numpy(prev))
-    pt.render(spp)
+    pt.render(spp, collect_stats=True)
     torch.cuda.synchronize()
     out = {k: pt.buffers.get(k).cpu().numpy() for k in ("pt accum buffer", "final result", "albedo", "normal", "test")}
     out["stats"] = pt.stats()
@@ -123,8 +123,8 @@ def test_cornell_parity_config1():
         assert np.array_equal(gpu[k], ref[rk]), k
     assert np.array_equal(gpu["test"].reshape(-1), ref["test"])
     s, rs = gpu["stats"], ref["stats"]
-    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
-        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
+    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"], s["shadow_rays_reference"]) == \
+        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"], rs["shadow_rays_reference"])
 
 
 def test_config1_cornellbox_named_size():
@@ -143,8 +143,10 @@ def test_config1_cornellbox_named_size():
     assert np.array_equal(gpu["pt accum buffer"].view(np.uint32), ref["accum"].view(np.uint32))
     assert np.array_equal(gpu["albedo"], ref["albedo"]) and np.array_equal(gpu["normal"], ref["normal"])
     s, rs = gpu["stats"], ref["stats"]
-    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
-        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
+    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"], s["shadow_rays_reference"]) == \
+        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"], rs["shadow_rays_reference"])
+    # the reference traces a shadow ray on every loop iteration past RR (main.cu:119-123)
+    assert rs["shadow_rays"] <= rs["shadow_rays_reference"] <= rs["primary_rays"] * (d.max_depth - 1)
 
 
 @pytest.mark.parametrize("accel", ["flat", "two_level"])
@@ -458,3 +460,90 @@ def test_render_from_another_thread():
     t.join(timeout=60)
     pt.close_engine()
     assert "img" in out and np.array_equal(out["img"], main)
+
+
+def test_camera_change_uploads_new_sensor():
+    """CameraChange after World.set_sensor: the pass re-reads the sensor and renders
+    exactly what a fresh engine on the moved camera renders (pt_pass.cpp:40-49)."""
+    import torch
+    from pupiloptixlab_amd.pt_pass import PTPass, Events
+    from pupiloptixlab_amd import world as W
+
+    w = _cornell(64)
+    pt = PTPass(device=0)
+    pt.set_scene(w)
+    pt.render(2)
+    torch.cuda.synchronize()
+    before = pt.buffers.get("pt accum buffer").cpu().numpy()
+    w.set_sensor(40.0, W.look_at_mitsuba((0.3, 1.2, 3.5), (0.0, 0.9, 0.0), (0.0, 1.0, 0.0)), fov_axis="x")
+    pt.events.dispatch(Events.CAMERA_CHANGE)
+    pt.render(2)
+    torch.cuda.synchronize()
+    moved = pt.buffers.get("pt accum buffer").cpu().numpy()
+    pt.close_engine()
+    fresh = render_gpu(w.desc(), 2)["pt accum buffer"]
+    assert not np.array_equal(before, moved)
+    assert np.array_equal(moved.view(np.uint32), fresh.view(np.uint32))
+    ref = oracle.OracleScene(w.desc()).render(spp=2)["accum"]
+    assert np.array_equal(moved.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("accel", ["flat", "two_level"])
+def test_skewed_scene_stays_within_stack_capacity(accel, monkeypatch):
+    """A geometric chain of triangles (size and spacing x1.15 per triangle) makes the
+    nearest-neighbour PLOC build a caterpillar far deeper than the traversal stacks
+    hold; create() detects the depth and rebuilds with the Morton-bounded Karras
+    LBVH, so every traversal variant still returns the oracle's hits."""
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    monkeypatch.setenv("PUPIL_ACCEL", accel)
+    n = 300
+    a = 1.15 ** np.arange(n)
+    pos = np.zeros((n, 3, 3), np.float32)
+    pos[:, 0] = np.stack([a, np.zeros(n), np.zeros(n)], 1)
+    pos[:, 1] = np.stack([a + 0.5 * a, np.zeros(n), np.zeros(n)], 1)
+    pos[:, 2] = np.stack([a, 0.5 * a, 0.25 * a], 1)
+    w = World()
+    s = w.add_mesh(pos.reshape(-1, 3), np.arange(3 * n, dtype=np.uint32).reshape(-1, 3))
+    w.add_instance(s, w.add_material(world_mod.diffuse((0.5, 0.5, 0.5))))
+    w.set_film(16, 16, 2)
+    w.set_sensor(40.0, world_mod.look_at_mitsuba((0, 0, -3), (0, 0, 0), (0, 1, 0)))
+    desc = w.desc()
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    depth = pt.stats()["bvh_depth"]
+    pt.close_engine()
+    assert 0 < depth and 3 * depth + 2 <= 176, depth  # kRing + kStackOvf entries, 3 per level
+    rng = np.random.default_rng(9)
+    m = 20000
+    tgt = pos[rng.integers(0, n, m)].mean(axis=1) + rng.normal(0, 0.05, (m, 3)) * a[rng.integers(0, n, m)][:, None]
+    org = rng.uniform(-2, 2, (m, 3)) + np.array([0, 0, -5.0])
+    d = tgt - org
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([org, d], 1).astype(np.float32)
+    ref = oracle.OracleScene(desc).closest(rays)
+    assert (ref[:, 0] > 0).sum() > 1000
+    for width, refill in TRAVERSALS if accel == "flat" else [("4", "24")]:
+        monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+        monkeypatch.setenv("PUPIL_REFILL", refill)
+        out = _trace(desc, rays)
+        bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
+        assert not bad.any(), f"{accel} bvh{width} refill {refill}: {bad.sum()} rays differ"
+
+
+def test_render_rejects_max_depth_above_128():
+    """The C ABI refuses max_depth > 128 (PTPass's inspector range, pt_pass.cpp:225-237)
+    instead of silently under-counting rays past the per-bounce log."""
+    import ctypes as C
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    pt = PTPass(device=0)
+    pt.set_scene(_cornell(16).desc())
+    la = abi.Launch()
+    la.spp, la.max_depth, la.accumulate, la.tile_size, la.tile_world = 1, 129, 1, 32, 1
+    f = pt._frame()
+    assert pt._lib.pupil_pt_render(pt._pt, C.byref(f), C.byref(la), None) == abi.ERR_INVALID
+    la.max_depth = 128
+    assert pt._lib.pupil_pt_render(pt._pt, C.byref(f), C.byref(la), None) == 0
+    pt.stats()
+    pt.close_engine()

@@ -60,10 +60,18 @@ def traffic_json(root, kernels, out_path, note=""):
     f, w = pooled("FETCH_SIZE"), pooled("WRITE_SIZE")
     hit, miss = pooled("TCC_HIT_sum"), pooled("TCC_MISS_sum")
     d = [x for k in ks for x in dur[k]]
-    rec = {"kernel": " + ".join(ks), "fetch_size_kib": f, "write_size_kib": w,
+    avg_ms = sum(d) / len(d) / 1e6
+    valu, grbm = pooled("SQ_INSTS_VALU"), pooled("GRBM_GUI_ACTIVE")
+    rec = {"kernel": " + ".join(ks), "round": os.environ.get("PUPIL_ROUND", ""),
+           "fetch_size_kib": f, "write_size_kib": w,
            "traffic_bytes_per_launch": (2.0 * f + w) * 1024.0,
            "l2_hit_rate": hit / max(1.0, hit + miss),
-           "avg_ms_under_pmc": sum(d) / len(d) / 1e6, "note": note}
+           "avg_ms_under_pmc": avg_ms,
+           # VALU issue: SQ_INSTS_VALU wave-instructions; GRBM_GUI_ACTIVE is summed over the
+           # 8 XCDs, so the engine clock is GRBM / 8 / launch time
+           "valu_insts_per_launch": valu or None,
+           "clock_ghz": (grbm / 8.0 / (avg_ms * 1e-3) / 1e9) if grbm else None,
+           "note": note}
     with open(out_path, "w") as fh:
         json.dump(rec, fh, indent=1)
     print(json.dumps(rec))
