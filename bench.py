@@ -51,6 +51,9 @@ def parse():
                     help="CPU baseline renders every k-th pixel (default: full frame for configs 3/4, 1/16 for 5)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every CPU this process may run on, capped by the cgroup quota)")
+    ap.add_argument("--dropin", type=int, default=1,
+                    help="also time the C++ drop-in cadence (build/pupil_path_tracer: spp x PTPass::OnRun of 1 spp, "
+                         "each synchronised) on the same scene exported as XML + OBJ (rank 0, N=1, configs 3/4)")
     ap.add_argument("--save", default="", help="write the frame as PNG (rank 0)")
     ap.add_argument("--dump", default="", help="write the full float32 frame as .npy (rank 0, after the timed steps)")
     args = ap.parse_args()
@@ -176,6 +179,10 @@ def main():
     # rate / the gather ceiling measured on this box by build/ubench_gather), VALU
     # issue and HBM bytes (both from the committed PMC passes of this config).
     roof = roofline(args, st_bytes, trace_ms, trace_launches) if rank == 0 else None
+    dropin = None
+    if rank == 0 and world == 1 and args.dropin and args.config in (3, 4):
+        dropin = dropin_cadence(args, ms_per_step, mrays)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         cpu = cpu_baseline(desc, args, pt)
@@ -232,12 +239,42 @@ def main():
                        "stage_ms_per_frame": {"primary_extend": round(ext_ms, 3),
                                               "bounce_trace": round(trace_ms - ext_ms, 3),
                                               "shade": round(shade_ms, 3)}},
+            "dropin_cpp": dropin,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dropin_cadence(args, batched_ms, batched_mrays):
+    """The reference's cadence through the C++ drop-in: examples/path_tracer (System +
+    PTPass, pt_pass.cpp:39-57: one 1-spp launch per OnRun, then a stream sync) on
+    this scene exported as XML + OBJ (scenes.XmlWorld; loads bit-identically)."""
+    import subprocess
+    import tempfile
+
+    from pupiloptixlab_amd import scenes
+
+    exe = os.path.join(HERE, "build", "pupil_path_tracer")
+    if not os.path.exists(exe):
+        return {"error": "build/pupil_path_tracer not built"}
+    with tempfile.TemporaryDirectory() as tmp:
+        xw = scenes.XmlWorld()
+        scenes.sphere_field(args.spheres, args.width, args.height, args.max_depth, seed=1, world=xw)
+        path = xw.save(os.path.join(tmp, f"config{args.config}.xml"))
+        env = dict(os.environ, PUPIL_BENCH=f"2,{max(3, args.steps)},{args.spp}")
+        try:
+            r = subprocess.run([exe, path], capture_output=True, text=True, timeout=600, env=env)
+            rec = json.loads(r.stdout.strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError, subprocess.SubprocessError) as e:
+            return {"error": f"{type(e).__name__}: {e}"}
+    rec["vs_batched_ms"] = round(rec["ms_per_frame"] / batched_ms, 3) if batched_ms > 0 else None
+    rec["what"] = (f"{args.spp} x C++ PTPass::OnRun (1 spp + hipStreamSynchronize each) per frame, "
+                   "examples/path_tracer on the exported XML; value/ms_per_step above batch the frame's spp "
+                   "in one launch sequence")
+    return rec
 
 
 def default_config(args):

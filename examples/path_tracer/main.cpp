@@ -5,6 +5,8 @@
 // util::BitmapTexture::Save, or .pfm).
 //
 // usage: pupil_path_tracer <scene.xml> [frames=16] [out.exr|.hdr|.pfm] [device=0]
+//        PUPIL_BENCH=warmup,frames,spp pupil_path_tracer <scene.xml>   (drop-in cadence benchmark)
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -13,6 +15,43 @@
 #include "pupil/denoiser.h"
 #include "pupil/framework.h"
 #include "pupil/pt_pass.h"
+
+// PUPIL_BENCH="warmup,frames,spp": the drop-in cadence of the reference
+// (pt_pass.cpp:39-57): a frame is `spp` x System::Run(1), i.e. spp x
+// PTPass::OnRun of 1 spp each with its stream synchronisation; each frame
+// restarts accumulation through a CameraChange event.  One untimed frame
+// counts the rays (pupil_pt_stats after every OnRun); then `warmup` untimed
+// and `frames` timed frames (steady_clock around the whole loop).  Prints one
+// JSON line.
+static int Bench(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spec) {
+    int warmup = 1, frames = 5, spp = 8;
+    if (std::sscanf(spec, "%d,%d,%d", &warmup, &frames, &spp) != 3 || frames < 1 || spp < 1) {
+        std::fprintf(stderr, "PUPIL_BENCH must be warmup,frames,spp\n");
+        return 2;
+    }
+    auto frame = [&]() {
+        Pupil::EventDispatcher<Pupil::EWorldEvent::CameraChange>();
+        system.Run((uint32_t)spp);
+    };
+    Pupil::EventDispatcher<Pupil::EWorldEvent::CameraChange>();
+    double rays = 0.0;
+    for (int k = 0; k < spp; k++) {
+        system.Run(1);
+        pupil_pt_counters c{};
+        if (!pass.Stats(c)) return 1;
+        rays += (double)(c.primary_rays + c.extension_rays + c.shadow_rays);
+    }
+    for (int k = 0; k < warmup; k++) frame();
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < frames; k++) frame();
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("{\"ms_per_frame\": %.4f, \"onrun_ms\": %.4f, \"mrays_per_s\": %.2f, \"rays_per_frame\": %.0f, "
+                "\"frames\": %d, \"warmup\": %d, \"spp\": %d}\n",
+                1e3 * s / frames, 1e3 * s / (frames * spp), rays * frames / s / 1e6, rays, frames, warmup, spp);
+    return 0;
+}
 
 int main(int argc, char **argv) {
     if (argc < 2) {
@@ -30,6 +69,8 @@ int main(int argc, char **argv) {
         system->AddPass(pt_pass.get());
         if (!system->SetScene(argv[1])) {
             rc = 1;
+        } else if (const char *bench = std::getenv("PUPIL_BENCH")) {
+            rc = Bench(*system, *pt_pass, bench);
         } else {
             system->Run((uint32_t)frames);
             pt_pass->Inspector();

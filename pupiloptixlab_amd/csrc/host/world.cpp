@@ -152,12 +152,25 @@ bool LoadObj(const std::string &path, Mesh &out, std::string &err) {
     };
     std::vector<Corner> corners;
     bool any_t = false, any_n = false;
+    // assimp's OBJ importer makes one aiMesh per object ('o') and per material change
+    // ('usemtl') that receives faces; the reference loads a file only when it yields
+    // exactly one mesh (resource/shape.cpp:230-233), so count them the same way.
+    int meshes = 0;
+    bool segment_has_faces = false;
+    std::string material;
     std::string line;
     while (std::getline(f, line)) {
         std::istringstream ss(line);
         std::string tag;
         ss >> tag;
-        if (tag == "v") {
+        if (tag == "o") {
+            segment_has_faces = false;
+        } else if (tag == "usemtl") {
+            std::string m;
+            ss >> m;
+            if (m != material && segment_has_faces) segment_has_faces = false;
+            material = m;
+        } else if (tag == "v") {
             float x, y, z;
             ss >> x >> y >> z;
             v.insert(v.end(), {x, y, z});
@@ -193,12 +206,21 @@ bool LoadObj(const std::string &path, Mesh &out, std::string &err) {
                 c.n = fix(parts[2], vn.size() / 3);
                 poly.push_back(c);
             }
+            if (!segment_has_faces && poly.size() >= 3) {
+                segment_has_faces = true;
+                meshes++;
+            }
             for (size_t k = 2; k < poly.size(); k++) {
                 corners.push_back(poly[0]);
                 corners.push_back(poly[k - 1]);
                 corners.push_back(poly[k]);
             }
         }
+    }
+    if (meshes != 1) {
+        err = path + " holds " + std::to_string(meshes) +
+              " meshes (objects / materials); only single-mesh OBJ files load (resource/shape.cpp:230-233)";
+        return false;
     }
     for (auto &c : corners) {
         if (c.t > 0) any_t = true;

@@ -19,6 +19,7 @@ import os
 
 import numpy as np
 
+from . import abi
 from . import world as W
 
 # data/static/cornellbox.xml transforms (row-major to_world of each shape)
@@ -163,12 +164,13 @@ def _field_geometry(num_spheres: int, seed: int, box=10.0):
 
 
 def sphere_field(num_spheres=500, width=1920, height=1080, max_depth=4, seed=1, slices=40, stacks=26,
-                 merge=True) -> W.World:
+                 merge=True, world=None) -> W.World:
     """Configs 3/4: ``num_spheres`` x 2,000-triangle spheres (+2 floor, +2 light triangles).
 
     With ``merge`` the spheres are baked into one world-space mesh (one
-    instance, like a single OBJ); otherwise one instance per sphere."""
-    wd = W.World()
+    instance, like a single OBJ); otherwise one instance per sphere.  ``world``
+    (e.g. an XmlWorld) receives the builder calls instead of a new World."""
+    wd = W.World() if world is None else world
     wd.set_film(width, height, max_depth)
     box = 10.0
     centers, radii, albedo = _field_geometry(num_spheres, seed, box)
@@ -226,6 +228,111 @@ def _room_and_light(wd: W.World):
                     emitter_radiance=(40.0, 38.0, 34.0))
     cam = W.look_at_mitsuba((0.0, 6.0, 13.0), (0.0, 4.6, 0.0), (0, 1, 0))
     wd.set_sensor(50.0, cam, fov_axis="y")
+
+
+class XmlWorld:
+    """Records the World-builder calls of a procedural scene and writes it as a
+    mitsuba-style XML file plus one OBJ per mesh, the input format of the
+    reference's example/path_tracer (System::SetScene(path)).  Matrices are
+    written as exact float32 <matrix> values, so loading the XML gives the same
+    scene description bit for bit.  Supports what the generators here use:
+    meshes, the rectangle builtin, diffuse (+twosided) materials, area emitters
+    and the perspective sensor."""
+
+    RECT = -1
+
+    def __init__(self):
+        self.film = (256, 256, 4)
+        self.sensor = None
+        self.meshes, self.materials, self.instances = [], [], []
+
+    def set_film(self, width, height, max_depth):
+        self.film = (int(width), int(height), int(max_depth))
+
+    def set_sensor(self, fov, to_world, fov_axis="x", near_clip=0.01, far_clip=10000.0):
+        self.sensor = (float(fov), np.asarray(to_world, np.float32).reshape(16), fov_axis, near_clip, far_clip)
+
+    def add_mesh(self, positions, indices, normals=None, texcoords=None):
+        self.meshes.append((np.asarray(positions, np.float32).reshape(-1, 3),
+                            np.asarray(indices, np.uint32).reshape(-1, 3),
+                            None if normals is None else np.asarray(normals, np.float32).reshape(-1, 3),
+                            None if texcoords is None else np.asarray(texcoords, np.float32).reshape(-1, 2)))
+        return len(self.meshes) - 1
+
+    def add_builtin(self, name):
+        if name != "rectangle":
+            raise ValueError("XmlWorld writes the rectangle builtin only")
+        return self.RECT
+
+    def add_material(self, m):
+        if m.type != abi.MAT_DIFFUSE or m.tex[0].type != abi.TEX_RGB:
+            raise ValueError("XmlWorld writes RGB diffuse materials only")
+        self.materials.append((tuple(m.tex[0].c0), bool(m.twosided)))
+        return len(self.materials) - 1
+
+    def add_instance(self, shape, material, to_world=None, flip_normals=False, flip_tex_coords=False,
+                     emitter_radiance=None):
+        if flip_normals:
+            raise ValueError("XmlWorld does not write flip_normals")
+        m = np.eye(4, dtype=np.float32) if to_world is None else np.asarray(to_world, np.float32).reshape(4, 4)
+        rad = None if emitter_radiance is None else tuple(float(x) for x in np.broadcast_to(emitter_radiance, 3))
+        self.instances.append((shape, material, m, bool(flip_tex_coords), rad))
+        return len(self.instances) - 1
+
+    @staticmethod
+    def _f(x):
+        return "%.9g" % float(x)
+
+    def save(self, path: str) -> str:
+        import os
+
+        root = os.path.dirname(os.path.abspath(path))
+        os.makedirs(root, exist_ok=True)
+        stem = os.path.splitext(os.path.basename(path))[0]
+        f = self._f
+        for k, (P, I, N, T) in enumerate(self.meshes):
+            with open(os.path.join(root, f"{stem}_mesh{k}.obj"), "w") as fh:
+                fh.write("".join(f"v {f(a)} {f(b)} {f(c)}\n" for a, b, c in P))
+                if T is not None:
+                    fh.write("".join(f"vt {f(a)} {f(b)}\n" for a, b in T))
+                if N is not None:
+                    fh.write("".join(f"vn {f(a)} {f(b)} {f(c)}\n" for a, b, c in N))
+                J = I + 1
+                if T is not None and N is not None:
+                    fh.write("".join(f"f {a}/{a}/{a} {b}/{b}/{b} {c}/{c}/{c}\n" for a, b, c in J))
+                elif N is not None:
+                    fh.write("".join(f"f {a}//{a} {b}//{b} {c}//{c}\n" for a, b, c in J))
+                else:
+                    fh.write("".join(f"f {a} {b} {c}\n" for a, b, c in J))
+        w, h, depth = self.film
+        out = ['<scene version="3.0.0">', f'  <integrator type="path"><integer name="max_depth" value="{depth}"/></integrator>']
+        if self.sensor is not None:
+            fov, m, axis, nc, fc = self.sensor
+            out += [f'  <sensor type="perspective"><float name="fov" value="{f(fov)}"/>'
+                    f'<string name="fov_axis" value="{axis}"/><float name="near_clip" value="{f(nc)}"/>'
+                    f'<float name="far_clip" value="{f(fc)}"/>',
+                    '    <transform name="to_world"><matrix value="' + " ".join(f(x) for x in m) + '"/></transform>',
+                    f'    <film type="hdrfilm"><integer name="width" value="{w}"/><integer name="height" value="{h}"/></film>',
+                    '  </sensor>']
+        for shape, mat, m, flip_tc, rad in self.instances:
+            if shape == self.RECT:
+                out.append('  <shape type="rectangle">')
+            else:
+                out.append(f'  <shape type="obj"><string name="filename" value="{stem}_mesh{shape}.obj"/>'
+                           f'<boolean name="flip_tex_coords" value="{"true" if flip_tc else "false"}"/>')
+            c, two = self.materials[mat]
+            bsdf = f'<bsdf type="diffuse"><rgb name="reflectance" value="{f(c[0])}, {f(c[1])}, {f(c[2])}"/></bsdf>'
+            out.append("    " + (f'<bsdf type="twosided">{bsdf}</bsdf>' if two else bsdf))
+            out.append('    <transform name="to_world"><matrix value="' + " ".join(f(x) for x in m.reshape(-1)) +
+                       '"/></transform>')
+            if rad is not None:
+                out.append(f'    <emitter type="area"><rgb name="radiance" value="{f(rad[0])}, {f(rad[1])}, '
+                           f'{f(rad[2])}"/></emitter>')
+            out.append("  </shape>")
+        out.append("</scene>")
+        with open(path, "w") as fh:
+            fh.write("\n".join(out) + "\n")
+        return path
 
 
 def blas_mesh(num_spheres=125, seed=2, box=4.0, slices=40, stacks=26):

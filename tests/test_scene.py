@@ -142,6 +142,26 @@ def test_obj_loader(tmp_path):
     assert d.instances[0].flip_tex_coords == 1  # OBJ default (shape.cpp:138)
 
 
+def test_obj_with_several_meshes_is_skipped(tmp_path):
+    """assimp splits an OBJ into one mesh per object / material; the reference loads
+    only single-mesh files (resource/shape.cpp:230-233) and skips the shape otherwise."""
+    quad = "v 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\n"
+    cases = {"two_objects": quad + "o a\nf 1 2 3\no b\nf 1 3 4\n",
+             "two_materials": quad + "usemtl red\nf 1 2 3\nusemtl blue\nf 1 3 4\n",
+             "one_object_one_material": quad + "o a\nusemtl red\nf 1 2 3\nf 1 3 4\n",
+             "same_material_twice": quad + "usemtl red\nf 1 2 3\nusemtl red\nf 1 3 4\n"}
+    faces = {}
+    for name, text in cases.items():
+        (tmp_path / f"{name}.obj").write_text(text)
+        p = tmp_path / f"{name}.xml"
+        p.write_text(f'<scene><shape type="obj"><string name="filename" value="{name}.obj"/>'
+                     '<bsdf type="diffuse"/></shape><shape type="rectangle"><bsdf type="diffuse"/></shape></scene>')
+        d = World().load_scene(str(p)).desc()
+        faces[name] = [d.shapes[d.instances[i].shape].num_faces for i in range(d.num_instances)]
+    assert faces["two_objects"] == [2] and faces["two_materials"] == [2]  # only the rectangle is left
+    assert faces["one_object_one_material"] == [2, 2] and faces["same_material_twice"] == [2, 2]
+
+
 def test_missing_file_is_io_error():
     with pytest.raises(abi.PupilError) as e:
         World().load_scene("/nonexistent/scene.xml")
@@ -173,3 +193,20 @@ def test_env_map_and_bitmap_textures_load(tmp_path):
     kinds = [(d.materials[i].tex[0].type, d.materials[i].tex[0].filter) for i in range(d.num_materials)]
     assert (abi.TEX_BITMAP, 0) in kinds and (abi.TEX_BITMAP, 1) in kinds
     assert any(d.materials[i].tex[1].type == abi.TEX_CHECKERBOARD for i in range(d.num_materials))
+
+
+def test_xml_export_of_procedural_field_loads_identically(tmp_path):
+    """scenes.XmlWorld writes a generator's scene as XML + OBJ (the example's input
+    format); loading it renders bit-identically to the programmatic scene."""
+    import oracle
+    from pupiloptixlab_amd import scenes
+
+    xw = scenes.XmlWorld()
+    scenes.sphere_field(12, 48, 32, 4, seed=3, world=xw)
+    path = xw.save(str(tmp_path / "field.xml"))
+    a = scenes.sphere_field(12, 48, 32, 4, seed=3).desc()
+    b = World().load_scene(path).desc()
+    assert (a.num_instances, a.num_area_emitters) == (b.num_instances, b.num_area_emitters)
+    ra = oracle.OracleScene(a).render(spp=2)["accum"]
+    rb = oracle.OracleScene(b).render(spp=2)["accum"]
+    assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32))

@@ -1,0 +1,15 @@
+#!/bin/bash
+# The C++ drop-in cadence (examples/path_tracer, PUPIL_BENCH) on config 4 and a
+# rocprofv3 kernel trace of it (per-launch timeline of 8 x 1-spp OnRun).
+set -u
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/dropin
+cd $R
+python3 tools/export_xml.py gpurun_out/dropin/config4.xml 4 || exit 1
+PUPIL_BENCH=2,5,8 timeout -k 10 300 build/pupil_path_tracer gpurun_out/dropin/config4.xml > gpurun_out/dropin/bench.log 2>&1
+rc=$?; echo "dropin rc=$rc"; tail -n 1 gpurun_out/dropin/bench.log
+[ "$rc" -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp
+PUPIL_BENCH=1,2,8 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/dropin/prof -o run --output-format csv -- $R/build/pupil_path_tracer $R/gpurun_out/dropin/config4.xml > $R/gpurun_out/dropin/prof.log 2>&1
+rc=$?; echo "rocprof rc=$rc"
+exit $rc
