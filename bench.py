@@ -129,7 +129,7 @@ def main():
 
     # one instrumented frame for the traversal byte counts (untimed)
     pt.mark_dirty()
-    pt.render(args.spp, collect_stats=True, stream=stream)
+    pt.render(args.spp, collect_stats=1, stream=stream)
     torch.cuda.synchronize(dev)
     st_bytes = pt.stats()
 
@@ -151,7 +151,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    st = pt.stats()  # stage timings (HIP events) of the last timed frame
+    # one more frame, untimed, with HIP events around every stage launch (the timed
+    # frames record none: each event adds ~6 us of stream gap) for the stage times
+    frame_timed = pt.stats()
+    pt.mark_dirty()
+    pt.render(args.spp, collect_stats=2, stream=stream)
+    torch.cuda.synchronize(dev)
+    st = pt.stats()
+    assert (st["primary_rays"], st["extension_rays"], st["shadow_rays"]) == \
+        (frame_timed["primary_rays"], frame_timed["extension_rays"], frame_timed["shadow_rays"])
     rays_frame = st["primary_rays"] + st["extension_rays"] + st["shadow_rays"]
     assert rays_frame == st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"]
     rays_local = rays_frame * args.steps

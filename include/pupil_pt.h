@@ -197,9 +197,16 @@ typedef struct pupil_pt_launch {
     uint32_t tile_size;
     uint32_t tile_rank;
     uint32_t tile_world;
-    uint32_t collect_stats; /* count node visits / triangle tests (slower) */
+    /* bit 0 (PUPIL_STATS_COUNTERS): count node visits / primitive tests and the
+     * reference's shadow-ray count (slower kernels); bit 1 (PUPIL_STATS_TIMING): HIP
+     * events around every stage launch for pupil_pt_stats' per-stage times (each
+     * event costs ~6 us of stream gap, so production frames leave it off) */
+    uint32_t collect_stats;
     uint32_t pad;
 } pupil_pt_launch;
+
+#define PUPIL_STATS_COUNTERS 1u
+#define PUPIL_STATS_TIMING 2u
 
 typedef struct pupil_pt_counters {
     uint64_t primary_rays;

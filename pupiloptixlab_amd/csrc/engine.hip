@@ -114,6 +114,9 @@ struct pupil_pt {
     std::vector<uint8_t> pair_kind;        // per pair: 0 extend, 1 shadow, 2 shade
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     uint32_t trace_pairs = 0;
+    // PUPIL_TRACE_TAIL: per-wave start / drained / exit times of each traversal launch of a stats render
+    unsigned long long *tail_buf = nullptr;
+    uint32_t tail_waves = 0, tail_launches = 0;
     pupil_pt_counters totals{};
     // scene tables kept for dynamic updates (pupil_pt_update_instance / _update_emitters)
     std::vector<DevInstance> h_insts;
@@ -698,11 +701,22 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     fp.albedo = (float *)out->albedo;
     fp.normal = (float *)out->normal;
     fp.test = (float *)out->test;
-    fp.nee_count = launch->collect_stats ? pt->trace_counters + 16 : nullptr;
+    const bool stats = (launch->collect_stats & PUPIL_STATS_COUNTERS) != 0;
+    const bool timing = (launch->collect_stats & PUPIL_STATS_TIMING) != 0;
+    fp.nee_count = stats ? pt->trace_counters + 16 : nullptr;
 
-    const bool stats = launch->collect_stats != 0;
     TraceStats ts_dev{pt->trace_counters};
     const TraceStats *tsp = stats ? &ts_dev : nullptr;
+    const bool tail = stats && std::getenv("PUPIL_TRACE_TAIL");
+    if (tail && !pt->tail_buf) {
+        pt->tail_waves = pt->ovf_threads / 64u;
+        if (pt->alloc(&pt->tail_buf, (size_t)(kMaxDepth + 1) * pt->tail_waves * 4)) return fail(PUPIL_ERR_OOM, "tail buffer");
+    }
+    if (tail) HIP_TRY(hipMemsetAsync(pt->tail_buf, 0, sizeof(unsigned long long) * (kMaxDepth + 1) * pt->tail_waves * 4, s));
+    pt->tail_launches = 0;
+    auto tail_slot = [&]() {  // wave-time slice of the next traversal launch
+        if (tail) ts_dev.wave_times = pt->tail_buf + (size_t)pt->tail_launches++ * pt->tail_waves * 4;
+    };
     const uint32_t bounces = fp.max_depth;
     // events: begin/end + one pair per stage launch (kind 0 extend, 1 shadow, 2 shade)
     const uint32_t pairs_needed = 3 * bounces + 1;
@@ -713,11 +727,15 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     }
     pt->pair_kind.assign(pairs_needed, 0);
     uint32_t pair = 0;
+    // stage events only on request: each hipEventRecord between two kernels costs
+    // ~6 us of stream gap (9 per 1-spp render at D = 4)
     auto ev0 = [&](uint8_t kind) {
+        if (!timing) return;
         pt->pair_kind[pair] = kind;
         (void)hipEventRecord(pt->trace_events[2 * pair], s);
     };
     auto ev1 = [&]() {
+        if (!timing) return;
         (void)hipEventRecord(pt->trace_events[2 * pair + 1], s);
         pair++;
     };
@@ -737,6 +755,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     // flags partition logs the per-bounce ray counts.
     launch_generate(pt->sc, fp, pt->ps, s);
     ev0(0);
+    tail_slot();
     launch_extend(pt->sc, pt->ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s);
     ev1();
     bin_paths();
@@ -753,6 +772,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
                              q.counts + kStartNext, nullptr, b < 128 ? pt->ray_log + 2 * b : nullptr, s);
             if (pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill) {
                 ev0(1);
+                tail_slot();
                 launch_trace_mixed(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);
                 ev1();
             } else {
@@ -808,6 +828,34 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
         c.extend_ms = kind_ms[0];
         c.extend_launches = kind_n[0];
         c.shade_ms = kind_ms[2];
+        if (pt->last_stats && pt->tail_buf && pt->tail_launches) {  // PUPIL_TRACE_TAIL summary on stderr
+            std::vector<unsigned long long> tb((size_t)pt->tail_launches * pt->tail_waves * 4);
+            HIP_TRY(hipMemcpy(tb.data(), pt->tail_buf, sizeof(unsigned long long) * tb.size(), hipMemcpyDeviceToHost));
+            for (uint32_t l = 0; l < pt->tail_launches; l++) {
+                const unsigned long long *w = tb.data() + (size_t)l * pt->tail_waves * 4;
+                std::vector<double> st, dr, ex;
+                unsigned long long t0 = ~0ull, rays = 0;
+                for (uint32_t k = 0; k < pt->tail_waves; k++)
+                    if (w[4 * k + 2]) t0 = std::min(t0, w[4 * k]);
+                for (uint32_t k = 0; k < pt->tail_waves; k++) {
+                    if (!w[4 * k + 2]) continue;
+                    st.push_back((double)(w[4 * k] - t0) * 0.01);  // 100 MHz -> us
+                    dr.push_back(w[4 * k + 1] ? (double)(w[4 * k + 1] - t0) * 0.01 : -1.0);
+                    ex.push_back((double)(w[4 * k + 2] - t0) * 0.01);
+                    rays += w[4 * k + 3];
+                }
+                if (ex.empty()) continue;
+                auto pct = [](std::vector<double> v, double q) {
+                    std::sort(v.begin(), v.end());
+                    return v[std::min(v.size() - 1, (size_t)(q * (double)v.size()))];
+                };
+                std::fprintf(stderr,
+                             "[pupil tail] launch %u: %zu waves, %llu rays; start p50 %.1f max %.1f us; drained "
+                             "first %.1f p50 %.1f us; exit p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f us\n",
+                             l, ex.size(), rays, pct(st, 0.5), pct(st, 1.0), pct(dr, 0.0), pct(dr, 0.5), pct(ex, 0.1),
+                             pct(ex, 0.5), pct(ex, 0.9), pct(ex, 0.99), pct(ex, 1.0));
+            }
+        }
         if (pt->last_stats) {
             unsigned long long tc[32];
             HIP_TRY(hipMemcpy(tc, pt->trace_counters, sizeof(tc), hipMemcpyDeviceToHost));

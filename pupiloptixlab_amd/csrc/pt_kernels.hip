@@ -622,6 +622,8 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     // workgroups round-robin over the XCDs) and move on to the next chunk when
     // theirs is exhausted, so every item is taken exactly once.
     uint32_t shard = blockIdx.x % kWorkShards, tried = 0;
+    unsigned long long t_start = 0, t_drained = 0, n_taken = 0;  // PUPIL_TRACE_TAIL
+    if (STATS && stats.wave_times) t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t p = 0, best_key = 0, best_idx = kMissIndex;
     RayPre r{};
     float tmin = 0.f, tmax = 0.f, b1 = 0.f, b2 = 0.f;
@@ -659,9 +661,13 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 dg[4]++;
                 dg[5] += min(n_idle, base < len ? len - base : 0u);
             }
+            if (STATS) n_taken += min(n_idle, base < len ? len - base : 0u);
             if (base + n_idle >= len) {  // chunk exhausted: continue on the next one
                 shard = shard + 1 == kWorkShards ? 0u : shard + 1;
-                if (++tried == kWorkShards) drained = true;
+                if (++tried == kWorkShards) {
+                    drained = true;
+                    if (STATS && stats.wave_times) t_drained = __builtin_amdgcn_s_memrealtime();
+                }
             }
             if (!active) {
                 const uint32_t k = base + (uint32_t)__popcll(idle & lanemask_lt());
@@ -856,6 +862,13 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     }
     flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
     if (MODE == kModeMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
+    if (STATS && stats.wave_times && lane_id() == 0) {
+        unsigned long long *w = stats.wave_times + 4ull * (blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u);
+        w[0] = t_start;
+        w[1] = t_drained;
+        w[2] = __builtin_amdgcn_s_memrealtime();
+        w[3] = n_taken;
+    }
     // the last wave out resets the counters for the next launch (no memset per
     // launch).  Waves count out on kWorkShards sub-counters (blockIdx % shards),
     // the last of each sub-counter on the final one: the exit burst at the end

@@ -206,8 +206,9 @@ class PTPass(Pass):
         f.compact = 1 if self.tile[2] > 1 else 0
         return f
 
-    def render(self, spp: int = 1, collect_stats: bool = False, stream=None):
-        """spp consecutive OnRun frames in one wavefront batch (asynchronous)."""
+    def render(self, spp: int = 1, collect_stats: int = 0, stream=None):
+        """spp consecutive OnRun frames in one wavefront batch (asynchronous).
+        collect_stats: bit 0 counters (node visits, ...), bit 1 per-stage HIP events."""
         if self.dirty:  # pt_pass.cpp:40-49: camera re-uploaded, accumulation restarted
             if self._world is not None:
                 d = self._world.desc()

@@ -50,7 +50,10 @@ def main():
             torch.cuda.synchronize()
             per_rank.append((time.perf_counter() - t0) / args.frames * 1e3)
             host_ms.append(host / args.frames * 1e3)
-            if r == 0:
+            if r == 0:  # one more frame with stage events for the stage times
+                pt.mark_dirty()
+                pt.render(8, collect_stats=2, stream=s)
+                torch.cuda.synchronize()
                 st = pt.stats()
                 stage0 = {"trace_ms": round(st["trace_ms"], 3), "trace_launches": st["trace_launches"],
                           "shade_ms": round(st["shade_ms"], 3),
