@@ -277,6 +277,15 @@ int pupil_debug_math(int device, uint32_t n, const float *x, const float *y2, fl
 enum { PUPIL_IMAGE_AUTO = 0, PUPIL_IMAGE_EXR = 1, PUPIL_IMAGE_HDR = 2, PUPIL_IMAGE_PFM = 3 };
 int pupil_image_save(const char *path, uint32_t width, uint32_t height, const float *rgba, uint32_t format);
 
+/* ---- image input (util::BitmapTexture::Load, framework/util/texture.cpp:87-174) ----
+ * Decodes an EXR (by the exact extension ".exr": tinyexr LoadEXR semantics), a
+ * Radiance HDR (by signature), a PNG or baseline JPEG (stbi_load semantics with the
+ * reference's pow(v / 255, 2.2) mapping) or a PFM file into float RGBA, row 0 = image
+ * top (the texture order).  Call with rgba = NULL to get the size, then with a
+ * buffer of width*height*4 floats.  PUPIL_ERR_IO with pupil_last_error() when the
+ * file is unreadable or its format is not supported. */
+int pupil_image_load(const char *path, uint32_t *width, uint32_t *height, float *rgba);
+
 /* ---- denoiser (substitute for optix::Denoiser, framework/optix/denoiser.h:7-66) ----
  * The OptiX AI denoiser has no ROCm equivalent; this is an edge-avoiding
  * a-trous wavelet filter (Dammertz et al. 2010): five passes of a 5x5 B3-spline

@@ -52,6 +52,10 @@ std::vector<std::string> split(const std::string &s, const std::string &delims) 
 float to_float(const std::string &s) { return std::stof(s); }
 }  // namespace
 
+namespace image {  // image_load.cpp
+bool LoadBitmap(const std::string &path, std::vector<float> &rgba, int &w, int &h, std::string &err);
+}
+
 namespace resource {
 
 struct Texture {
@@ -255,29 +259,14 @@ bool LoadObj(const std::string &path, Mesh &out, std::string &err) {
     return true;
 }
 
-// PFM reader (bitmap textures / env maps); other formats fall back to black
-// like TextureManager::GetTexture on a load failure (resource/texture.cpp:53-60).
-bool LoadPfm(const std::string &path, Texture &t) {
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return false;
-    std::string magic;
-    int w, h;
-    float scale;
-    f >> magic >> w >> h >> scale;
-    f.get();
-    if ((magic != "PF" && magic != "Pf") || w <= 0 || h <= 0) return false;
-    const int ch = magic == "PF" ? 3 : 1;
-    std::vector<float> raw((size_t)w * h * ch);
-    f.read(reinterpret_cast<char *>(raw.data()), raw.size() * sizeof(float));
-    if (!f) return false;
-    auto data = std::make_shared<std::vector<float>>((size_t)w * h * 4, 1.f);
-    // PFM rows are stored bottom-to-top; keep image row 0 = top like stb/tinyexr
-    for (int y = 0; y < h; y++)
-        for (int x = 0; x < w; x++) {
-            const size_t src = ((size_t)(h - 1 - y) * w + x) * ch;
-            const size_t dst = ((size_t)y * w + x) * 4;
-            for (int k = 0; k < 3; k++) (*data)[dst + k] = raw[src + (ch == 3 ? k : 0)];
-        }
+// util::BitmapTexture::Load (framework/util/texture.cpp:162-174) -> a bitmap
+// texture; EXR / HDR / PNG / JPEG / PFM decoding lives in image_load.cpp.
+// On failure the caller falls back to black like TextureManager::GetTexture
+// (resource/texture.cpp:53-60).
+bool LoadImageTexture(const std::string &path, Texture &t, std::string &err) {
+    auto data = std::make_shared<std::vector<float>>();
+    int w = 0, h = 0;
+    if (!Pupil::image::LoadBitmap(path, *data, w, h, err)) return false;
     t.type = PUPIL_TEX_BITMAP;
     t.width = (uint32_t)w;
     t.height = (uint32_t)h;
@@ -478,8 +467,9 @@ public:
         if (o->type == "bitmap") {
             const auto path = (root / o->GetProperty("filename")).string();
             Texture loaded;
-            if (!LoadPfm(path, loaded)) {
-                warn("bitmap [" + path + "] not loadable (PFM only); using black");
+            std::string err;
+            if (!LoadImageTexture(path, loaded, err)) {
+                warn("bitmap [" + path + "] not loadable (" + err + "); using black");
                 loaded = ColorTexture({0, 0, 0});
             }
             t = loaded;
@@ -674,8 +664,9 @@ public:
                     e.type = PUPIL_EMITTER_ENV_MAP;
                     LoadFloat(o, "scale", e.scale, 1.f);
                     const auto path = (root / o->GetProperty("filename")).string();
-                    if (!LoadPfm(path, e.envmap)) {
-                        warn("env map [" + path + "] not loadable (PFM only); skipped");
+                    std::string err;
+                    if (!LoadImageTexture(path, e.envmap, err)) {
+                        warn("env map [" + path + "] not loadable (" + err + "); skipped");
                         continue;
                     }
                     e.envmap.filter = 1;

@@ -388,12 +388,15 @@ def _write_pfm(path: str, rgb: np.ndarray):
         f.write(np.ascontiguousarray(rgb[::-1], dtype="<f4").tobytes())
 
 
-def textured_env_xml(path: str, width=320, height=240, max_depth=5, seed=4) -> str:
+def textured_env_xml(path: str, width=320, height=240, max_depth=5, seed=4, env_format="pfm",
+                     tex_format="pfm") -> str:
     """Scene-input fidelity scene: an env-map emitter
-    (PFM, rotated, scaled; world/emitter.cpp:107-149 CDF), bitmap textures with
+    (rotated, scaled; world/emitter.cpp:107-149 CDF), bitmap textures with
     point and bilinear filtering and a to_uv scale (cuda/texture.cpp:60-102),
     a checkerboard, a small area light, open sky so the env map is seen and
-    sampled.  The PFM files are written next to the XML."""
+    sampled.  The image files are written next to the XML: the env map as
+    env_format ("pfm", "exr" or "hdr", the latter two by pupil_image_save), the
+    bitmap as tex_format ("pfm", or "png" / "jpg" 8-bit through PIL)."""
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
     rng = np.random.Generator(np.random.PCG64(seed))
@@ -401,8 +404,23 @@ def textured_env_xml(path: str, width=320, height=240, max_depth=5, seed=4) -> s
     yy, xx = np.mgrid[0:eh, 0:ew].astype(np.float32)
     env = np.stack([0.3 + 0.7 * (1 - yy / eh), 0.4 + 0.3 * np.sin(xx / ew * 6.283), 0.5 + 0.5 * yy / eh], -1)
     env[4:7, 40:44] = (30.0, 25.0, 18.0)  # a sun
-    _write_pfm(os.path.join(d, "env.pfm"), env.astype(np.float32))
-    _write_pfm(os.path.join(d, "tex.pfm"), rng.uniform(0.1, 0.9, (16, 16, 3)).astype(np.float32))
+    tex = rng.uniform(0.1, 0.9, (16, 16, 3)).astype(np.float32)
+    env_file, tex_file = f"env.{env_format}", f"tex.{tex_format}"
+    if env_format == "pfm":
+        _write_pfm(os.path.join(d, env_file), env.astype(np.float32))
+    else:
+        import ctypes as C
+
+        rgba = np.concatenate([env, np.ones((eh, ew, 1), np.float32)], -1).astype(np.float32)
+        fmt = {"exr": 1, "hdr": 2}[env_format]
+        abi.check(abi.load_library().pupil_image_save(os.path.join(d, env_file).encode(), ew, eh,
+                                                      rgba.ctypes.data_as(abi.f32p), fmt))
+    if tex_format == "pfm":
+        _write_pfm(os.path.join(d, tex_file), tex)
+    else:
+        from PIL import Image
+
+        Image.fromarray((tex * 255).astype(np.uint8), "RGB").save(os.path.join(d, tex_file), quality=90)
     lines = [
         '<scene version="3.0.0">',
         f'  <integrator type="path"><integer name="max_depth" value="{max_depth}"/></integrator>',
@@ -411,15 +429,15 @@ def textured_env_xml(path: str, width=320, height=240, max_depth=5, seed=4) -> s
         f'    <film type="hdrfilm"><integer name="width" value="{width}"/><integer name="height" value="{height}"/>'
         '</film>',
         '  </sensor>',
-        '  <emitter type="envmap"><string name="filename" value="env.pfm"/><float name="scale" value="1.5"/>',
+        f'  <emitter type="envmap"><string name="filename" value="{env_file}"/><float name="scale" value="1.5"/>',
         '    <transform name="to_world"><rotate y="1" angle="30"/></transform></emitter>',
         '  <shape type="rectangle"><transform name="to_world"><scale x="6" y="6" z="1"/>'
         '<rotate x="1" angle="-90"/></transform>',
-        '    <bsdf type="diffuse"><texture type="bitmap" name="reflectance"><string name="filename" value="tex.pfm"/>'
+        f'    <bsdf type="diffuse"><texture type="bitmap" name="reflectance"><string name="filename" value="{tex_file}"/>'
         '<string name="filter_type" value="nearest"/><transform name="to_uv"><scale x="3" y="3"/></transform>'
         '</texture></bsdf></shape>',
         '  <shape type="sphere"><point name="center" x="-1.2" y="1" z="0"/><float name="radius" value="1"/>',
-        '    <bsdf type="diffuse"><texture type="bitmap" name="reflectance"><string name="filename" value="tex.pfm"/>'
+        f'    <bsdf type="diffuse"><texture type="bitmap" name="reflectance"><string name="filename" value="{tex_file}"/>'
         '<string name="filter_type" value="bilinear"/></texture></bsdf></shape>',
         '  <shape type="sphere"><point name="center" x="1.2" y="0.8" z="0.3"/><float name="radius" value="0.8"/>',
         '    <bsdf type="roughplastic"><float name="alpha" value="0.2"/><float name="int_ior" value="1.5"/>'

@@ -432,6 +432,20 @@ def test_env_map_and_bitmap_textures_parity():
         assert np.array_equal(gpu[k], ref[k])
 
 
+@pytest.mark.parametrize("env_format,tex_format", [("exr", "png"), ("hdr", "jpg")])
+def test_env_map_and_bitmap_file_formats_parity(env_format, tex_format):
+    """The same scene with the env map as EXR / Radiance HDR and the bitmap as PNG /
+    JPEG (util::BitmapTexture::Load, texture.cpp:87-174): the decoded textures are
+    sampled on the GPU bit-identically to the oracle."""
+    p = scenes.textured_env_xml(os.path.join(TMP, f"texenv_{env_format}", "texenv.xml"), 160, 120, 5,
+                                env_format=env_format, tex_format=tex_format)
+    desc = World().load_scene(p).desc()
+    assert desc.env and desc.env.contents.radiance.type == abi.TEX_BITMAP
+    gpu = render_gpu(desc, 4)
+    ref = oracle.OracleScene(desc).render(spp=4)
+    assert compare(gpu, ref, f"texenv-{env_format}-{tex_format}") == 160 * 120
+
+
 def test_render_from_another_thread():
     """SURVEY §8(b) threading: PTPass::OnRun runs on a render thread other than the one that
     created the engine (system.cpp:93-106); every call sets its HIP device, so a render issued
