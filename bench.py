@@ -41,6 +41,9 @@ def parse():
                          "5 = 40 x 250k-tri instanced rough dielectric/plastic field, 3840x2160 16 spp D6")
     ap.add_argument("--spheres", type=int, default=None, help="spheres in the field (configs 3/4) or per BLAS (5)")
     ap.add_argument("--instances", type=int, default=40, help="config 5 instances")
+    ap.add_argument("--emissive-groups", type=int, default=0,
+                    help="configs 3/4: make that many of the 8 sphere groups emissive (one area emitter per "
+                         "triangle; an emissive-mesh workload for NEE emitter selection)")
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
@@ -96,7 +99,8 @@ def main():
         scene = scenes.instanced_field(args.instances, args.width, args.height, args.max_depth, seed=2,
                                        spheres_per_blas=args.spheres)
     else:
-        scene = scenes.sphere_field(args.spheres, args.width, args.height, args.max_depth, seed=1)
+        scene = scenes.sphere_field(args.spheres, args.width, args.height, args.max_depth, seed=1,
+                                    emissive_groups=args.emissive_groups)
     desc = scene.desc()
     n_prims = tris = 0
     for i in range(desc.num_instances):
@@ -188,11 +192,11 @@ def main():
     # issue and HBM bytes (both from the committed PMC passes of this config).
     roof = roofline(args, st_bytes, trace_ms, trace_launches) if rank == 0 else None
     dropin = None
-    if rank == 0 and world == 1 and args.dropin and args.config in (3, 4):
+    if rank == 0 and world == 1 and args.dropin and args.config in (3, 4) and args.emissive_groups == 0:
         dropin = dropin_cadence(args, ms_per_step, mrays)
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline:
+    if rank == 0 and world == 1 and args.cpu_baseline and args.emissive_groups == 0:
         cpu = cpu_baseline(desc, args, pt)
 
     if rank == 0:
@@ -222,6 +226,8 @@ def main():
                                     f"{'instanced field' if args.config == 5 else 'sphere field'} ({tris:,} tris), "
                                     f"{args.width}x{args.height}, {args.spp} spp, max_depth {args.max_depth}"),
                        "frame": f"{args.spp} x PTPass::OnRun", "parallelism": f"tiles{args.tile}x{world}",
+                       "area_emitters": int(desc.num_area_emitters),
+                       "emitter_select": os.environ.get("PUPIL_EMITTER_SELECT", "guide"),
                        "rays_per_frame": rays_total / args.steps,
                        # shadow rays the reference would trace (one per loop iteration past RR,
                        # main.cu:119-123); the engine and the oracle trace one only when the
@@ -287,7 +293,8 @@ def dropin_cadence(args, batched_ms, batched_mrays):
 
 def default_config(args):
     defaults = {3: (125, 1920, 1080, 8, 4), 4: (500, 1920, 1080, 8, 4), 5: (125, 3840, 2160, 16, 6)}
-    return (args.spheres, args.width, args.height, args.spp, args.max_depth) == defaults[args.config]
+    return (args.spheres, args.width, args.height, args.spp, args.max_depth) == defaults[args.config] and \
+        args.emissive_groups == 0
 
 
 def pmc_record(args):

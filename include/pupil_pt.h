@@ -269,6 +269,9 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
 /* evaluates the device's sin, cos, acos, atan2(x, y2), sqrt, 1/x on n inputs:
  * out[6*i + k] for k in that order (bit-exactness probe for the CPU oracle) */
 int pupil_debug_math(int device, uint32_t n, const float *x, const float *y2, float *out);
+/* the device's emitter pick (EmitterGroup::SelectOneEmiiter, render/emitter.h:110-135)
+ * for n random numbers p: out[i] = area emitter index, -1 = env, -2 = none */
+int pupil_debug_select_emitter(pupil_pt *pt, uint32_t n, const float *p, int32_t *out);
 
 /* ---- image output (util::BitmapTexture::Save, framework/util/texture.cpp:12-85,152-160) ----
  * rgba: width*height float4, row 0 = image bottom (the "final result" order).

@@ -118,6 +118,7 @@ SIGNATURES = {
     "pupil_pt_trace_rays": (C.c_int, [C.c_void_p, C.c_uint32, f32p, f32p, C.c_int]),
     "pupil_debug_math": (C.c_int, [C.c_int, C.c_uint32, f32p, f32p, f32p]),
     "pupil_image_save": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, f32p, C.c_uint32]),
+    "pupil_debug_select_emitter": (C.c_int, [C.c_void_p, C.c_uint32, f32p, C.POINTER(C.c_int32)]),
     "pupil_image_load": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), f32p]),
     "pupil_world_create": (C.c_int, [C.POINTER(C.c_void_p)]),
     "pupil_world_load_xml": (C.c_int, [C.c_void_p, C.c_char_p]),

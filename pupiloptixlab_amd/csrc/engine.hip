@@ -125,6 +125,7 @@ struct pupil_pt {
     uint32_t *d_prim_inst = nullptr;
     DevEmitter *d_areas = nullptr, *d_env = nullptr;
     float *d_cdf = nullptr;
+    uint32_t *d_guide = nullptr;
 
     template <typename T>
     hipError_t alloc(T **p, size_t count) {
@@ -271,8 +272,26 @@ int upload_emitters(pupil_pt *pt, const pupil_scene_desc *scene) {
     }
     DevEmitter *d_areas = nullptr, *d_env = nullptr;
     float *d_cdf = nullptr;
+    uint32_t *d_guide = nullptr;
     if (pt->upload(&d_areas, areas.data(), areas.size()) || pt->upload(&d_cdf, cdf.data(), cdf.size()))
         return fail(PUPIL_ERR_OOM, "emitter upload failed");
+    // guide table: 2^bits >= emitter count buckets (at most 2^20), guide[k] = first i
+    // with cdf[i] >= k / 2^bits (PUPIL_EMITTER_SELECT=binary: plain binary search, A/B)
+    uint32_t bits = 0;
+    while ((1u << bits) < scene->num_area_emitters && bits < 20) bits++;
+    const char *sel = std::getenv("PUPIL_EMITTER_SELECT");
+    const bool guide = scene->num_area_emitters > 1 && !(sel && std::strcmp(sel, "binary") == 0);
+    if (guide) {
+        const uint32_t m = 1u << bits;
+        std::vector<uint32_t> g(m + 1);
+        uint32_t i = 0;
+        for (uint32_t k = 0; k <= m; k++) {
+            const float t = (float)k / (float)m;
+            while (i < cdf.size() && cdf[i] < t) i++;
+            g[k] = i;
+        }
+        if (pt->upload(&d_guide, g.data(), g.size())) return fail(PUPIL_ERR_OOM, "emitter guide upload failed");
+    }
     if (scene->env && scene->env->type != PUPIL_EMITTER_NONE) {
         DevEmitter env;
         int rc = convert_emitter(pt, *scene->env, env);
@@ -282,8 +301,12 @@ int upload_emitters(pupil_pt *pt, const pupil_scene_desc *scene) {
     pt->release(pt->d_areas);
     pt->release(pt->d_cdf);
     pt->release(pt->d_env);
+    pt->release(pt->d_guide);
     pt->d_areas = d_areas;
     pt->d_cdf = d_cdf;
+    pt->d_guide = d_guide;
+    pt->sc.area_guide = d_guide;
+    pt->sc.guide_bits = bits;
     pt->d_env = d_env;
     pt->sc.areas = d_areas;
     pt->sc.area_cdf = d_cdf;
@@ -907,6 +930,27 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
     (void)hipFree(d_rays);
     if (d_out) (void)hipFree(d_out);
     HIP_TRY(e);
+    return PUPIL_OK;
+}
+
+int pupil_debug_select_emitter(pupil_pt *pt, uint32_t n, const float *p, int32_t *out) {
+    if (!pt || !p || !out) return fail(PUPIL_ERR_INVALID, "null argument");
+    if (n == 0) return PUPIL_OK;
+    HIP_TRY(hipSetDevice(pt->device));
+    HIP_TRY(hipDeviceSynchronize());
+    float *dp = nullptr;
+    int *dout = nullptr;
+    HIP_TRY(hipMalloc((void **)&dp, sizeof(float) * n));
+    hipError_t err = hipMalloc((void **)&dout, sizeof(int) * n);
+    if (err == hipSuccess) err = hipMemcpy(dp, p, sizeof(float) * n, hipMemcpyHostToDevice);
+    if (err == hipSuccess) {
+        launch_debug_select(pt->sc, dp, dout, n, pt->own_stream);
+        err = hipStreamSynchronize(pt->own_stream);
+    }
+    if (err == hipSuccess) err = hipMemcpy(out, dout, sizeof(int) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(dp);
+    if (dout) (void)hipFree(dout);
+    HIP_TRY(err);
     return PUPIL_OK;
 }
 

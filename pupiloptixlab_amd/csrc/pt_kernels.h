@@ -124,6 +124,8 @@ uint32_t trace_grid_blocks();
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
                         uint32_t ovf_threads, uint32_t *work, hipStream_t s);
 void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, hipStream_t s);
+// device emitter selection for n random numbers: area index, -1 env, -2 none
+void launch_debug_select(const DeviceScene &sc, const float *p, int *out, uint32_t n, hipStream_t s);
 
 // stable partition of path ids 0..n-1 by a key byte (queue_partition.hip)
 uint32_t partition_hist_entries(uint32_t n);

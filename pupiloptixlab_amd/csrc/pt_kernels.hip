@@ -1024,8 +1024,19 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, v
 
 // EmitterGroup::SelectOneEmiiter (render/emitter.h:110-135) as a binary search
 // over the sequentially accumulated CDF: picks the same emitter as the scan.
+// SelectOneEmiiter (render/emitter.h:110-135): the first area emitter i with
+// p <= cdf[i] (the linear scan's sum_p + select_probability, accumulated in the same
+// order), else the env emitter, else the last area emitter.  The guide table narrows
+// the search to the bucket of p (expected O(1) for any emitter count); the binary
+// search over that range returns exactly the linear scan's index.
 __device__ __forceinline__ const DevEmitter *select_emitter(const DeviceScene &sc, float p, float &sel_prob) {
     uint32_t lo = 0, hi = sc.num_areas;
+    if (sc.area_guide) {
+        const uint32_t m = 1u << sc.guide_bits;
+        const uint32_t k = min((uint32_t)(p * (float)m), m - 1u);  // exact: m is a power of two <= 2^24
+        lo = sc.area_guide[k];
+        hi = sc.area_guide[k + 1];
+    }
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if (p <= sc.area_cdf[mid]) hi = mid;
@@ -1369,6 +1380,18 @@ void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, ui
     }
     const uint32_t blocks = std::min((n + kTraceBlock - 1) / kTraceBlock, std::max(1u, ovf_threads / kTraceBlock));
     hipLaunchKernelGGL(k_trace_debug, dim3(blocks), dim3(kTraceBlock), 0, s, sc, rays, out, n, any, ovf, ovf_threads);
+}
+
+__global__ void k_debug_select(DeviceScene sc, const float *p, int *out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float prob;
+    const DevEmitter *e = select_emitter(sc, p[i], prob);
+    out[i] = !e ? -2 : (e == sc.env && sc.has_env ? -1 : (int)(e - sc.areas));
+}
+
+void launch_debug_select(const DeviceScene &sc, const float *p, int *out, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_debug_select, dim3((n + 255) / 256), dim3(256), 0, s, sc, p, out, n);
 }
 
 void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, hipStream_t s) {

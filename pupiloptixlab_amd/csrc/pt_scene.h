@@ -147,6 +147,11 @@ struct DeviceScene {
     const DevMaterial *materials;
     const DevEmitter *areas;
     const float *area_cdf;  // sequential CDF of select_probability (emitter.h:110-120)
+    // guide table over area_cdf (Chen & Asau's indexed search): area_guide[k] = first i
+    // with area_cdf[i] >= k / 2^guide_bits, k = 0..2^guide_bits, so the pick for p lies in
+    // [guide[k], guide[k+1]] with k = floor(p 2^guide_bits); null = plain binary search
+    const uint32_t *area_guide;
+    uint32_t guide_bits;
     uint32_t num_areas;
     uint32_t has_env;
     const DevEmitter *env;

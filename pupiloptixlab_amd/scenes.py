@@ -164,12 +164,15 @@ def _field_geometry(num_spheres: int, seed: int, box=10.0):
 
 
 def sphere_field(num_spheres=500, width=1920, height=1080, max_depth=4, seed=1, slices=40, stacks=26,
-                 merge=True, world=None) -> W.World:
+                 merge=True, world=None, emissive_groups=0) -> W.World:
     """Configs 3/4: ``num_spheres`` x 2,000-triangle spheres (+2 floor, +2 light triangles).
 
     With ``merge`` the spheres are baked into one world-space mesh (one
     instance, like a single OBJ); otherwise one instance per sphere.  ``world``
-    (e.g. an XmlWorld) receives the builder calls instead of a new World."""
+    (e.g. an XmlWorld) receives the builder calls instead of a new World.
+    ``emissive_groups`` (merged mode): that many of the 8 sphere groups become area
+    emitters, one emitter per triangle (world/emitter.cpp:169-222), i.e. an
+    emissive-mesh workload for NEE emitter selection."""
     wd = W.World() if world is None else world
     wd.set_film(width, height, max_depth)
     box = 10.0
@@ -199,7 +202,10 @@ def sphere_field(num_spheres=500, width=1920, height=1080, max_depth=4, seed=1, 
             ii = np.concatenate([idx + o for o in off])
             s = wd.add_mesh(pos, ii, nn, tt)
             m = wd.add_material(W.diffuse(tuple(albedo[sel[0]])))
-            wd.add_instance(s, m)
+            if g < emissive_groups:
+                wd.add_instance(s, m, emitter_radiance=(1.5 + 0.2 * g, 1.2, 0.9))
+            else:
+                wd.add_instance(s, m)
             mats.append(m)
     else:
         s = wd.add_mesh(v, idx, nrm, uv)

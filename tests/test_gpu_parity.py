@@ -561,3 +561,53 @@ def test_render_rejects_max_depth_above_128():
     assert pt._lib.pupil_pt_render(pt._pt, C.byref(f), C.byref(la), None) == 0
     pt.stats()
     pt.close_engine()
+
+
+def _emissive_field(spheres=24, w=96, h=64, groups=2):
+    return scenes.sphere_field(spheres, w, h, 4, seed=5, slices=12, stacks=8, emissive_groups=groups)
+
+
+@pytest.mark.parametrize("mode", ["guide", "binary"])
+def test_emitter_pick_equals_the_reference_linear_scan(mode, monkeypatch):
+    """SelectOneEmiiter (render/emitter.h:110-135) is a linear scan over the sequentially
+    accumulated select_probability; the device's guide table (and the binary search it
+    narrows) must return exactly that index for every p, including p equal to a CDF
+    entry, its float neighbours and the guide's bucket boundaries."""
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    monkeypatch.setenv("PUPIL_EMITTER_SELECT", mode)
+    desc = _emissive_field().desc()
+    n = desc.num_area_emitters
+    assert n > 500
+    prob = np.array([desc.area_emitters[i].select_probability for i in range(n)], np.float32)
+    cdf = np.zeros(n, np.float32)
+    s = np.float32(0.0)
+    for i in range(n):  # fl(sum_p + p_i), in order
+        cdf[i] = s + prob[i]
+        s = cdf[i]
+    rng = np.random.default_rng(3)
+    m = 1 << int(np.ceil(np.log2(n)))
+    p = np.concatenate([(rng.integers(0, 1 << 24, 200000) / float(1 << 24)).astype(np.float32), cdf,
+                        np.nextafter(cdf, np.float32(0)), np.nextafter(cdf, np.float32(2)),
+                        (np.arange(m + 1) / m).astype(np.float32),
+                        np.nextafter((np.arange(1, m + 1) / m).astype(np.float32), np.float32(0)),
+                        np.float32([0.0, (2 ** 24 - 1) / 2 ** 24])])
+    p = p[(p >= 0) & (p < 1)].astype(np.float32)
+    ref = np.searchsorted(cdf, p, side="left").astype(np.int64)  # first i with p <= cdf[i]
+    ref = np.where(ref >= n, n - 1, ref)  # no env: the last area emitter (emitter_cb)
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    out = np.zeros(len(p), np.int32)
+    abi.check(pt._lib.pupil_debug_select_emitter(pt._pt, len(p), np.ascontiguousarray(p).ctypes.data_as(abi.f32p),
+                                                 out.ctypes.data_as(abi.C.POINTER(abi.C.c_int32))))
+    pt.close_engine()
+    assert np.array_equal(out, ref), f"{(out != ref).sum()} picks differ"
+
+
+def test_emissive_mesh_render_parity():
+    """An emissive-mesh scene (two sphere groups emit, one emitter per triangle): NEE
+    selection, area sampling and MIS render bit-identically to the oracle."""
+    desc = _emissive_field().desc()
+    gpu = render_gpu(desc, 2)
+    ref = oracle.OracleScene(desc).render(spp=2)
+    assert compare(gpu, ref, "emissive-mesh") == desc.width * desc.height
