@@ -47,9 +47,12 @@ static int Bench(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spe
     for (int k = 0; k < frames; k++) frame();
     if (hipDeviceSynchronize() != hipSuccess) return 1;
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    std::printf("{\"ms_per_frame\": %.4f, \"onrun_ms\": %.4f, \"mrays_per_s\": %.2f, \"rays_per_frame\": %.0f, "
-                "\"frames\": %d, \"warmup\": %d, \"spp\": %d}\n",
-                1e3 * s / frames, 1e3 * s / (frames * spp), rays * frames / s / 1e6, rays, frames, warmup, spp);
+    Pupil::FrameGather *g = system.Gather();
+    if (g && g->Info().rank != 0) return 0;
+    std::printf("{\"ms_per_frame\": %.4f, \"onrun_ms\": %.4f, \"mrays_per_s_rank0\": %.2f, \"rays_per_frame_rank0\": %.0f, "
+                "\"frames\": %d, \"warmup\": %d, \"spp\": %d, \"ranks\": %d}\n",
+                1e3 * s / frames, 1e3 * s / (frames * spp), rays * frames / s / 1e6, rays, frames, warmup, spp,
+                g ? g->Info().world : 1);
     return 0;
 }
 
@@ -62,6 +65,14 @@ int main(int argc, char **argv) {
     const char *out = argc > 3 ? argv[3] : "";
     auto system = Pupil::util::Singleton<Pupil::System>::instance();
     system->device = argc > 4 ? std::atoi(argv[4]) : 0;
+    // multi-GPU (pupil/dist.h): one process per GPU with torchrun's RANK / WORLD_SIZE /
+    // LOCAL_RANK; PUPIL_DIST=1 forces the RCCL path for a single rank
+    const Pupil::DistInfo dist = Pupil::DistFromEnv();
+    const char *force = std::getenv("PUPIL_DIST");
+    if ((dist.world > 1 || (force && std::atoi(force))) && !system->InitDistributed(dist)) {
+        std::fprintf(stderr, "rank %d: RCCL initialisation failed\n", dist.rank);
+        return 1;
+    }
     system->Init(false);
     int rc = 0;
     {
@@ -78,7 +89,11 @@ int main(int argc, char **argv) {
             auto *buf = bm->GetBuffer(Pupil::BufferManager::DEFAULT_FINAL_RESULT_BUFFER_NAME);
             const int w = system->GetWorld()->scene->sensor.film.w, h = system->GetWorld()->scene->sensor.film.h;
             const char *dn = std::getenv("PUPIL_DENOISE");  // optix::Denoiser substitute on the final result
-            if (buf && dn && std::atoi(dn)) {
+            if (dist.rank != 0) {  // the gathered frame lives on rank 0
+                system->Destroy();
+                return 0;
+            }
+            if (buf && dn && std::atoi(dn) && !system->Gather()) {
                 Pupil::optix::Denoiser denoiser(Pupil::optix::Denoiser::UseAlbedo | Pupil::optix::Denoiser::UseNormal);
                 denoiser.Setup((unsigned)w, (unsigned)h);
                 Pupil::optix::Denoiser::ExecutionData data;

@@ -1,0 +1,66 @@
+// dist.h — multi-GPU sharding of the drop-in (BASELINE.json north_star: image-space
+// tiles across the GPUs of one node, scene replicated in HBM, per-tile radiance
+// gathered over RCCL).  The reference is single-GPU; each pixel's path depends only
+// on (pixel_index, random_seed) and the read-only scene (example/path_tracer/
+// main.cu:40,53), so ranks render disjoint tile sets of the same frame and the
+// result is bit-identical to one GPU.
+//
+// One process per GPU, launched like torchrun does (RANK, WORLD_SIZE, LOCAL_RANK,
+// MASTER_PORT in the environment).  Tile t (32 x 32, row-major) belongs to rank
+// t % world (pupil_pt_local_pixels).  Once per OnRun every rank sends its compact
+// "final result" tiles to rank 0 (ncclSend / ncclRecv in one group: one message
+// per rank, ~4 MB at 1080p and 8 GPUs, over xGMI), and rank 0 scatters them into
+// its full-frame "final result" with one kernel.  No collective sits inside the
+// render; the gather is the only exchange.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace Pupil {
+
+struct DistInfo {
+    int rank = 0;
+    int world = 1;
+    int local_rank = 0;
+    uint32_t tile = 32;
+};
+
+// RANK / WORLD_SIZE / LOCAL_RANK (torchrun's variables); world = 1 without them.
+DistInfo DistFromEnv() noexcept;
+
+class FrameGather {
+public:
+    FrameGather() noexcept = default;
+    ~FrameGather() noexcept;
+    FrameGather(const FrameGather &) = delete;
+    FrameGather &operator=(const FrameGather &) = delete;
+
+    // Collective over all ranks: rank 0 creates the RCCL unique id and hands it to
+    // the others through `id_path` (a file on the node's local filesystem, written
+    // atomically); every rank then joins the communicator on `device`.
+    bool Init(const DistInfo &d, int device, const std::string &id_path) noexcept;
+    // Per frame size: the tile maps of every rank (rank 0 keeps them on the device).
+    bool Setup(uint32_t width, uint32_t height) noexcept;
+    // Gathers every rank's compact float4 buffer (this rank's `LocalPixels()` pixels,
+    // in map order) into rank 0's full float4 image on `stream`; asynchronous.
+    bool Gather(const void *local, void *full, hipStream_t stream) noexcept;
+
+    uint32_t LocalPixels() const noexcept { return m_counts.empty() ? 0u : m_counts[(size_t)m_info.rank]; }
+    const DistInfo &Info() const noexcept { return m_info; }
+
+private:
+    DistInfo m_info{};
+    ncclComm_t m_comm = nullptr;
+    uint32_t m_w = 0, m_h = 0;
+    std::vector<uint32_t> m_counts;   // pixels per rank
+    std::vector<uint32_t *> m_maps;   // rank 0: device pixel map per rank
+    std::vector<float *> m_staging;   // rank 0: received compact buffers per rank
+    void Release() noexcept;
+};
+
+}  // namespace Pupil

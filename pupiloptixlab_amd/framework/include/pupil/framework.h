@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../../../include/pupil_pt.h"
+#include "dist.h"
 
 namespace Pupil {
 
@@ -152,9 +153,17 @@ public:
     void Destroy() noexcept;
     world::World *GetWorld() noexcept { return m_world.get(); }
 
+    // Multi-GPU (dist.h): call before SetScene in every rank's process; selects
+    // device = local_rank and joins the RCCL communicator (also for world = 1, which
+    // then gathers to itself).  Passes render this rank's tiles and PTPass gathers
+    // the frame into rank 0's "final result".
+    bool InitDistributed(const DistInfo &d) noexcept;
+    FrameGather *Gather() noexcept { return m_gather.get(); }
+
 private:
     std::vector<Pass *> m_passes;
     std::unique_ptr<world::World> m_world;
+    std::unique_ptr<FrameGather> m_gather;
 };
 
 }  // namespace Pupil

@@ -36,6 +36,7 @@ private:
     hipStream_t m_stream = nullptr;
     world::World *m_world = nullptr;
     pupil_pt_frame m_frame{};
+    void *m_full_result = nullptr;  // System's full-frame "final result" (the gather target)
     uint32_t m_random_seed = 0;
     uint32_t m_sample_cnt = 0;
     uint32_t m_frame_max_depth = 1;  // value in effect for the running accumulation

@@ -100,9 +100,25 @@ bool System::SetScene(const std::filesystem::path &xml) noexcept {
     return SetScene(std::move(w));
 }
 
+bool System::InitDistributed(const DistInfo &d) noexcept {
+    device = d.local_rank;
+    auto g = std::make_unique<FrameGather>();
+    const char *id = std::getenv("PUPIL_RCCL_ID_FILE");
+    const char *port = std::getenv("MASTER_PORT");
+    const std::string path = id && *id ? std::string(id)
+                                       : "/tmp/pupil_rccl_" + std::string(port && *port ? port : "0") + ".id";
+    if (!g->Init(d, device, path)) return false;
+    m_gather = std::move(g);
+    return true;
+}
+
 bool System::SetScene(std::unique_ptr<world::World> w) noexcept {
     if (!w) return false;
     (void)hipSetDevice(device);
+    if (m_gather && !m_gather->Setup((uint32_t)w->scene->sensor.film.w, (uint32_t)w->scene->sensor.film.h)) {
+        Log("tile maps for the multi-GPU gather could not be set up");
+        return false;
+    }
     BufferDesc desc;
     desc.name = std::string(BufferManager::DEFAULT_FINAL_RESULT_BUFFER_NAME);
     desc.flag = EBufferFlag::AllowDisplay;
@@ -126,6 +142,7 @@ void System::Destroy() noexcept {
     EventDispatcher<ESystemEvent::Quit>();
     m_passes.clear();
     m_world.reset();
+    m_gather.reset();
     BufferManager::instance()->Destroy();
 }
 

@@ -35,8 +35,18 @@ void PTPass::OnRun() noexcept {
     launch.spp = 1;
     launch.max_depth = m_frame_max_depth;
     launch.accumulate = m_accumulated_flag ? 1u : 0u;
+    FrameGather *gather = util::Singleton<System>::instance()->Gather();
+    if (gather) {  // this rank's tiles only (dist.h)
+        launch.tile_size = gather->Info().tile;
+        launch.tile_rank = (uint32_t)gather->Info().rank;
+        launch.tile_world = (uint32_t)gather->Info().world;
+    }
     if (pupil_pt_render(m_engine, &m_frame, &launch, m_stream) != PUPIL_OK) {
         Log("%s: render failed: %s", name.c_str(), pupil_last_error());
+        return;
+    }
+    if (gather && !gather->Gather(m_frame.frame, m_full_result, m_stream)) {
+        Log("%s: tile gather failed", name.c_str());
         return;
     }
     (void)hipStreamSynchronize(m_stream);
@@ -51,11 +61,23 @@ void PTPass::SetScene(world::World *world) noexcept {
         pupil_pt_destroy(m_engine);
         m_engine = nullptr;
     }
-    const int w = world->scene->sensor.film.w, h = world->scene->sensor.film.h;
+    int w = world->scene->sensor.film.w, h = world->scene->sensor.film.h;
     m_max_depth = world->scene->integrator.max_depth;
     m_accumulated_flag = true;
     auto *bm = BufferManager::instance();
     Buffer *final_result = bm->GetBuffer(BufferManager::DEFAULT_FINAL_RESULT_BUFFER_NAME);
+    m_full_result = final_result ? final_result->cuda_ptr : nullptr;
+    FrameGather *gather = util::Singleton<System>::instance()->Gather();
+    if (gather) {  // multi-GPU: the pass's buffers hold this rank's tiles, compact (dist.h)
+        w = (int)std::max(1u, gather->LocalPixels());
+        h = 1;
+        BufferDesc tiles;
+        tiles.name = "final result (local tiles)";
+        tiles.width = (uint32_t)w;
+        tiles.height = 1;
+        tiles.stride_in_byte = sizeof(float) * 4;
+        final_result = bm->AllocBuffer(tiles);
+    }
     BufferDesc desc;
     desc.width = (uint32_t)w;
     desc.height = (uint32_t)h;
@@ -76,7 +98,7 @@ void PTPass::SetScene(world::World *world) noexcept {
         return;
     }
     m_frame = pupil_pt_frame{accum->cuda_ptr, final_result->cuda_ptr, albedo->cuda_ptr, normal->cuda_ptr,
-                             test->cuda_ptr, 0u, 0u};
+                             test->cuda_ptr, gather ? 1u : 0u, 0u};
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (pupil_pt_create(&world->Desc(), dev, &m_engine) != PUPIL_OK) {
