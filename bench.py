@@ -331,8 +331,9 @@ def gather_ceiling(bvh_nodes):
 
 
 def roofline(args, st_bytes, trace_ms, trace_launches):
-    launches = max(1, st_bytes["trace_launches"])
-    ms = trace_ms / max(1, trace_launches)  # HIP events on the render stream, last timed frame
+    # the counter frame records no stage events; its traversal launches are the timing frame's
+    launches = max(1, trace_launches)
+    ms = trace_ms / launches  # HIP events on the render stream, the extra timing frame
     sec = ms * 1e-3
     nodes = st_bytes["node_visits"] / launches
     alg_bytes = st_bytes["trace_bytes"] / launches
