@@ -19,8 +19,12 @@ struct TwoLevelAccel {
     Bvh4Node *nodes4 = nullptr;  // [0, tlas_cap) TLAS, then the rebased BLASes
     float4 *prims = nullptr;     // 3 float4 per BLAS primitive, object space, BLAS leaf order; w of [0] = local id
     float4 *attrs = nullptr;     // kAttrStride float4 per BLAS primitive, the mesh's own primitive order
+    float4 *wprims = nullptr;    // 3 float4 per (mesh instance, BLAS primitive): world vertices fl(to_world * v),
+                                 // instance-major, BLAS leaf order; w of [0] = global primitive id
+    uint32_t num_wprims = 0;
     float *d_boxes = nullptr;    // 6 floats per instance: world box
     uint32_t *d_list = nullptr, *d_verts = nullptr;  // scratch: instance list, vertices per instance
+    uint32_t *d_faces = nullptr;                     // BLAS primitives per instance (world records)
     uint32_t tlas_cap = 0, tlas_nodes = 0, num_nodes4 = 0, num_prims = 0;
     uint32_t tlas_depth = 0, blas_depth = 0;  // BVH4 levels (deepest BLAS); see kTraceStackEntries
     uint32_t root_link4 = (uint32_t)kTraverseDone;

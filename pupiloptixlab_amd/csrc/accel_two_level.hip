@@ -88,6 +88,31 @@ __global__ __launch_bounds__(kBlock) void k_inst_bounds(const DevInstance *insts
         }
 }
 
+// World-space triangle records of each listed mesh instance: its BLAS records'
+// vertices through fl(to_world * v) (the product the flattened build and the
+// oracle test), so the two-level leaf test needs no per-triangle transform.
+// Grid: x over the instance's primitives, y over the list.
+__global__ __launch_bounds__(kBlock) void k_world_records(const DevInstance *insts, const uint32_t *list,
+                                                          const uint32_t *num_prims, const float4 *obj, float4 *wrec) {
+    const uint32_t id = list[blockIdx.y];
+    const DevInstance &in = insts[id];
+    if (in.kind == PUPIL_SHAPE_SPHERE) return;
+    const uint32_t n = num_prims[id];
+    const uint32_t base = (uint32_t)((int32_t)in.attr_base);  // the shape's first BLAS record
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const float4 a = obj[3 * (size_t)(base + j) + 0];
+        const float4 b = obj[3 * (size_t)(base + j) + 1];
+        const float4 c = obj[3 * (size_t)(base + j) + 2];
+        const vec3 w0 = xform_point(in.to_world, v3(a.x, a.y, a.z));
+        const vec3 w1 = xform_point(in.to_world, v3(b.x, b.y, b.z));
+        const vec3 w2 = xform_point(in.to_world, v3(c.x, c.y, c.z));
+        float4 *o = wrec + 3 * (size_t)((int64_t)base + j + in.wrec_delta);
+        o[0] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(in.prim_offset + __float_as_uint(a.w)));
+        o[1] = make_float4(w1.x, w1.y, w1.z, 0.f);
+        o[2] = make_float4(w2.x, w2.y, w2.z, 0.f);
+    }
+}
+
 // Rebase the links of one BLAS copied into the combined node array.
 __global__ void k_relink(Bvh4Node *nodes, uint32_t count, uint32_t node_base, uint32_t prim_base) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -226,6 +251,9 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
             return -1;
         hipLaunchKernelGGL(k_inst_bounds, dim3((uint32_t)changed.size()), dim3(kBlock), 0, s, d_insts, acc.d_list,
                            acc.d_verts, acc.d_boxes);
+        if (acc.wprims)  // the changed instances' world-space triangle records
+            hipLaunchKernelGGL(k_world_records, dim3(256, (uint32_t)changed.size()), dim3(kBlock), 0, s, d_insts,
+                               acc.d_list, acc.d_faces, acc.prims, acc.wprims);
         std::vector<float> h(6 * (size_t)n);
         if (hipMemcpyAsync(h.data(), acc.d_boxes, sizeof(float) * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
@@ -359,8 +387,10 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     }
     acc.num_nodes4 = total_nodes;
     acc.num_prims = total_prims;
-    // per instance: BLAS root / record base / margin, then the world boxes and the TLAS
-    std::vector<uint32_t> verts(n, 0), all(n);
+    // per instance: BLAS root / record base / margin / world-record base, then the
+    // world records, the world boxes and the TLAS
+    std::vector<uint32_t> verts(n, 0), faces(n, 0), all(n);
+    uint64_t wbase = 0;
     for (uint32_t i = 0; i < n; i++) {
         all[i] = i;
         DevInstance &d = insts[i];
@@ -374,10 +404,21 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         d.blas_root = shapes[k].num_faces ? rebase_link((int)blas[k].root_link4, node_base[k], prim_base[k])
                                           : kTraverseDone;
         d.attr_base = prim_base[k];
+        d.wrec_delta = (int32_t)((int64_t)wbase - (int64_t)prim_base[k]);
+        wbase += shapes[k].num_faces;
         verts[i] = shapes[k].num_vertices;
+        faces[i] = shapes[k].num_faces;
         instance_margin(d, shapes[k].vmax);
     }
     int trc = 0;
+    if (wbase >= (1ull << 31) ||
+        hipMalloc((void **)&acc.wprims, sizeof(float4) * 3 * (size_t)std::max<uint64_t>(1, wbase)) != hipSuccess ||
+        hipMalloc((void **)&acc.d_faces, sizeof(uint32_t) * n) != hipSuccess ||
+        hipMemcpy(acc.d_faces, faces.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess) {
+        free_two_level(acc);
+        return -1;
+    }
+    acc.num_wprims = (uint32_t)wbase;
     if (hipMemcpy(acc.d_verts, verts.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_insts, insts.data(), sizeof(DevInstance) * n, hipMemcpyHostToDevice) != hipSuccess ||
         (trc = rebuild_tlas(acc, insts, d_insts, all, s)) != 0) {
@@ -389,7 +430,7 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
 }
 
 void free_two_level(TwoLevelAccel &acc) {
-    void *p[] = {acc.nodes4, acc.prims, acc.attrs, acc.d_boxes, acc.d_list, acc.d_verts};
+    void *p[] = {acc.nodes4, acc.prims, acc.attrs, acc.d_boxes, acc.d_list, acc.d_verts, acc.wprims, acc.d_faces};
     for (void *x : p)
         if (x) (void)hipFree(x);
     acc = TwoLevelAccel{};

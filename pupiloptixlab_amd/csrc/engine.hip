@@ -558,6 +558,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         sc.root_link = (uint32_t)kTraverseDone;
         sc.nodes4 = pt->tl.nodes4;
         sc.prims = pt->tl.prims;
+        sc.wprims = pt->tl.wprims;
         sc.attrs = pt->tl.attrs;
         sc.root_link4 = pt->tl.root_link4;
     } else {

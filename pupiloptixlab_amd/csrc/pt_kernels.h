@@ -10,7 +10,7 @@ namespace pupil {
 
 constexpr int kTraceBlock = 128;
 constexpr int kTraceWavesPerSimd = 7;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8: 2 % slower)
-constexpr int kTraceWavesPerSimdTL = 4;  // two-level variant (<= 128 VGPRs)
+constexpr int kTraceWavesPerSimdTL = 5;  // two-level variant (<= 96 VGPRs; A/B r02 on config 5: 4 waves 688, 5: 743, 6: 716 Mrays/s)
 constexpr int kStackLds = 32;   // per-thread LDS stack entries
 constexpr int kStackOvf = 160;  // per-thread global overflow entries
 constexpr int kRing = 16;       // persistent BVH4 kernels: per-lane LDS ring entries (spills to the overflow column)

@@ -198,20 +198,19 @@ __device__ __forceinline__ bool intersect_leaf_tl(const DeviceScene &sc, const R
                                                   float tmin, float &tmax, uint32_t &best_key, uint32_t &best_idx,
                                                   float &bb1, float &bb2, uint32_t &prims_tested, bool &found,
                                                   bool any) {
-    const DevInstance &in = sc.instances[inst];
+    // the instance's world-space records (fl(to_world * v), precomputed per instance):
+    // no per-triangle transform in the loop
+    const float4 *rec = sc.wprims + 3 * (int64_t)sc.instances[inst].wrec_delta;
     const uint32_t first = leaf_first(leaf);
     const uint32_t count = leaf_count(leaf);
     for (uint32_t i = first; i < first + count; i++) {
-        const float4 a = sc.prims[3 * i + 0];
-        const float4 b = sc.prims[3 * i + 1];
-        const float4 c = sc.prims[3 * i + 2];
-        const uint32_t key = in.prim_offset + __float_as_uint(a.w);
+        const float4 a = rec[3 * i + 0];
+        const float4 b = rec[3 * i + 1];
+        const float4 c = rec[3 * i + 2];
+        const uint32_t key = __float_as_uint(a.w);
         if (STATS) prims_tested++;
         float t, b1 = 0.f, b2 = 0.f;
-        const vec3 w0 = xform_point(in.to_world, v3(a.x, a.y, a.z));
-        const vec3 w1 = xform_point(in.to_world, v3(b.x, b.y, b.z));
-        const vec3 w2 = xform_point(in.to_world, v3(c.x, c.y, c.z));
-        if (intersect_triangle(r, w0, w1, w2, tmin, tmax, t, b1, b2)) {
+        if (intersect_triangle(r, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), tmin, tmax, t, b1, b2)) {
             if (any) {
                 found = true;
                 return true;

@@ -84,6 +84,7 @@ struct DevInstance {
     uint32_t bin;         // material bin of the instance's hits (0 miss, 1..7 EMatType, 8 unknown)
     float margin[2];      // object-space box margin: margin[0] * (|o| + t |d|) + margin[1]
     float wlo[3], whi[3];  // world box of the instance's world-space primitives
+    int32_t wrec_delta;    // world-space record of BLAS record i: wprims[3 * (i + wrec_delta)]
 };
 
 struct alignas(16) BvhNode {
@@ -142,6 +143,7 @@ struct DeviceScene {
     uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node
     uint32_t two_level;       // 1: nodes4 = TLAS over instances + object-space BLAS per shape;
                               //    prims/attrs = BLAS records, hit index = global primitive id
+    const float4 *wprims;       // two-level: per-instance world-space triangle records (see accel_two_level.hip)
     const uint32_t *prim_inst;  // global prim id -> instance
     const DevInstance *instances;
     const DevMaterial *materials;
