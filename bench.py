@@ -96,6 +96,9 @@ def main():
     from pupiloptixlab_amd.pt_pass import PTPass, FINAL_RESULT
 
     if args.config == 5:
+        # BASELINE config 5 names a two-level BVH (IAS -> GAS): the engine's world-mode
+        # two-level structure (PUPIL_ACCEL=flat for the flattened BVH, A/B)
+        os.environ.setdefault("PUPIL_ACCEL", "two_level")
         scene = scenes.instanced_field(args.instances, args.width, args.height, args.max_depth, seed=2,
                                        spheres_per_blas=args.spheres)
     else:
@@ -191,6 +194,18 @@ def main():
     # rate / the gather ceiling measured on this box by build/ubench_gather), VALU
     # issue and HBM bytes (both from the committed PMC passes of this config).
     roof = roofline(args, st_bytes, trace_ms, trace_launches) if rank == 0 else None
+    update = None
+    if args.config == 5 and rank == 0:  # RenderInstanceUpdate cost: move instance 0, re-sync the accel
+        from pupiloptixlab_amd import world as W
+
+        t0 = time.perf_counter()
+        scene.set_instance_transform(0, W.transform(translate=(0.25, 0.0, 0.0)) @
+                                     np.asarray(scene.desc().instances[0].to_world[:] + [0, 0, 0, 1],
+                                                np.float32).reshape(4, 4))
+        pt.update_instance(scene, 0)
+        torch.cuda.synchronize(dev)
+        update = {"host_ms": round((time.perf_counter() - t0) * 1e3, 3), "engine_ms": round(pt.stats()["build_ms"], 3)}
+
     dropin = None
     if rank == 0 and world == 1 and args.dropin and args.config in (3, 4) and args.emissive_groups == 0:
         dropin = dropin_cadence(args, ms_per_step, mrays)
@@ -227,6 +242,7 @@ def main():
                                     f"{args.width}x{args.height}, {args.spp} spp, max_depth {args.max_depth}"),
                        "frame": f"{args.spp} x PTPass::OnRun", "parallelism": f"tiles{args.tile}x{world}",
                        "area_emitters": int(desc.num_area_emitters),
+                       "accel": "two_level" if st_bytes["two_level"] else "flat",
                        "emitter_select": os.environ.get("PUPIL_EMITTER_SELECT", "guide"),
                        "rays_per_frame": rays_total / args.steps,
                        # shadow rays the reference would trace (one per loop iteration past RR,
@@ -254,6 +270,7 @@ def main():
                                               "bounce_trace": round(trace_ms - ext_ms, 3),
                                               "shade": round(shade_ms, 3)}},
             "dropin_cpp": dropin,
+            "instance_update_ms": update,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -2,6 +2,8 @@
 // one object-space BLAS per mesh shape); see accel_two_level.hip.
 #pragma once
 
+#include <array>
+#include <utility>
 #include <vector>
 
 #include "pt_kernels.h"
@@ -27,6 +29,19 @@ struct TwoLevelAccel {
     uint32_t *d_faces = nullptr;                     // BLAS primitives per instance (world records)
     uint32_t tlas_cap = 0, tlas_nodes = 0, num_nodes4 = 0, num_prims = 0;
     uint32_t tlas_depth = 0, blas_depth = 0;  // BVH4 levels (deepest BLAS); see kTraceStackEntries
+    // "world" mode (PUPIL_TL_MODE, default): every mesh instance gets a world-space copy of
+    // its shape's BLAS (child boxes transformed and re-quantised conservatively) and the
+    // TLAS is built over the nodes `braid` levels below each instance root, so the whole
+    // structure is one BVH4 the flat traversal kernels walk (no ray transform, no
+    // return markers, the flat kernel's occupancy).  HBM pays one BLAS copy per instance.
+    bool world = false;
+    uint32_t braid = 5;  // PUPIL_TL_BRAID
+    Bvh4Node *wnodes = nullptr;  // [0, tlas_cap) TLAS, then the per-instance world BLAS copies
+    float *d_wbox = nullptr;     // world box of every copied node (6 floats)
+    uint32_t num_wnodes = 0;
+    std::vector<std::vector<std::pair<int, std::array<float, 6>>>> entries;  // per instance: TLAS entries
+    std::vector<uint32_t> inst_shape;                  // shape of each instance (0xFFFFFFFF: sphere)
+    std::vector<std::vector<uint32_t>> shape_levels;   // per shape: BVH4 level starts of its BLAS (+ end)
     uint32_t root_link4 = (uint32_t)kTraverseDone;
     double build_ms = 0.0;
 };
@@ -50,5 +65,11 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
 int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstance *d_insts,
                  const std::vector<uint32_t> &changed, hipStream_t s);
 void free_two_level(TwoLevelAccel &acc);
+// BLAS box margins of an instance after its transform changed (uses its stored vmax)
+void refresh_instance_margins(DevInstance &d);
+// nodes of the traversed structure (object mode: TLAS + shared BLASes; world mode: TLAS + copies)
+inline uint64_t two_level_nodes(const TwoLevelAccel &a) {
+    return a.tlas_nodes + ((a.world ? a.num_wnodes : a.num_nodes4) - a.tlas_cap);
+}
 
 }  // namespace pupil

@@ -107,9 +107,75 @@ __global__ __launch_bounds__(kBlock) void k_world_records(const DevInstance *ins
         const vec3 w1 = xform_point(in.to_world, v3(b.x, b.y, b.z));
         const vec3 w2 = xform_point(in.to_world, v3(c.x, c.y, c.z));
         float4 *o = wrec + 3 * (size_t)((int64_t)base + j + in.wrec_delta);
+        // flat record format (bvh_build.hip k_prim_setup): a.w = global id, b.w = instance, c.w = material bin
         o[0] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(in.prim_offset + __float_as_uint(a.w)));
-        o[1] = make_float4(w1.x, w1.y, w1.z, 0.f);
-        o[2] = make_float4(w2.x, w2.y, w2.z, 0.f);
+        o[1] = make_float4(w1.x, w1.y, w1.z, __uint_as_float(id));
+        o[2] = make_float4(w2.x, w2.y, w2.z, __uint_as_float(in.bin));
+    }
+}
+
+// World-space copy of a mesh instance's BLAS (world mode), one BVH4 level per
+// launch from the deepest up: the node keeps the shared BLAS topology, and each
+// child box is refitted to the world geometry under it -- a leaf child's box is
+// the exact bounds of its world records fl(to_world * v), an inner child's box is
+// the world box its own copy got one launch earlier -- then quantised
+// conservatively.  Links move to the copy: inner links to wnode_base, leaf links
+// to the instance's world records (+ wrec_delta).  Records bounded exactly keep
+// the leaf test's hits; the boxes are as tight as a fresh world-space build of the
+// same topology (transforming object boxes would inflate every box it rotates).
+__global__ __launch_bounds__(kBlock) void k_world_refit(const DevInstance *insts, const uint32_t *inst,
+                                                        uint32_t lo, uint32_t hi, const Bvh4Node *obj,
+                                                        const float4 *wrec, Bvh4Node *wn, float *wbox) {
+    const DevInstance &in = insts[*inst];
+    for (uint32_t j = lo + blockIdx.x * blockDim.x + threadIdx.x; j < hi; j += gridDim.x * blockDim.x) {
+        const Bvh4Node n = obj[in.obj_nbase + j];
+        float clo[3][4], chi[3][4], nlo[3], nhi[3];
+        int link[4];
+        int nk = 0;
+        for (int a = 0; a < 3; a++) {
+            nlo[a] = __builtin_huge_valf();
+            nhi[a] = -__builtin_huge_valf();
+        }
+        for (int k = 0; k < 4; k++) {
+            const int l = n.child[k];
+            if (l == kEmptyLink) continue;
+            float bl[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+            float bh[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+            if (l >= 0) {
+                const int w = (int)(l - (int)in.obj_nbase + (int)in.wnode_base);
+                for (int a = 0; a < 3; a++) {
+                    bl[a] = wbox[6 * (size_t)w + a];
+                    bh[a] = wbox[6 * (size_t)w + 3 + a];
+                }
+                link[nk] = w;
+            } else {
+                const uint32_t first = (uint32_t)((int64_t)leaf_first(l) + in.wrec_delta), cnt = leaf_count(l);
+                for (uint32_t r = first; r < first + cnt; r++)
+                    for (int v = 0; v < 3; v++) {
+                        const float4 p = wrec[3 * (size_t)r + v];
+                        bl[0] = fminf(bl[0], p.x);
+                        bl[1] = fminf(bl[1], p.y);
+                        bl[2] = fminf(bl[2], p.z);
+                        bh[0] = fmaxf(bh[0], p.x);
+                        bh[1] = fmaxf(bh[1], p.y);
+                        bh[2] = fmaxf(bh[2], p.z);
+                    }
+                link[nk] = make_leaf(first, cnt);
+            }
+            for (int a = 0; a < 3; a++) {
+                clo[a][nk] = bl[a];
+                chi[a][nk] = bh[a];
+                nlo[a] = fminf(nlo[a], bl[a]);
+                nhi[a] = fmaxf(nhi[a], bh[a]);
+            }
+            nk++;
+        }
+        wn[in.wnode_base + j] = encode_bvh4(nlo, nhi, clo, chi, link, nk);
+        float *b = wbox + 6 * (size_t)(in.wnode_base + j);
+        for (int a = 0; a < 3; a++) {
+            b[a] = nlo[a];
+            b[3 + a] = nhi[a];
+        }
     }
 }
 
@@ -154,6 +220,50 @@ uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std
     int axis = 0;
     for (int k = 1; k < 3; k++)
         if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+    if (e - b > 1024) {  // large ranges (world-mode braided entries): binned SAH, O(n) per split
+        constexpr int kBins = 64;
+        const float lo = cb.lo[axis], ext = cb.hi[axis] - cb.lo[axis];
+        if (ext > 0.f) {
+            HostBox bb[kBins];
+            uint32_t cnt[kBins] = {};
+            for (auto &x : bb) x = HostBox::empty();
+            auto bin_of = [&](uint32_t id) {
+                const float c = 0.5f * (boxes[id].lo[axis] + boxes[id].hi[axis]);
+                return std::min(kBins - 1, std::max(0, (int)((c - lo) / ext * kBins)));
+            };
+            for (uint32_t i = b; i < e; i++) {
+                const int k = bin_of(ids[i]);
+                bb[k].grow(boxes[ids[i]]);
+                cnt[k]++;
+            }
+            float right[kBins];
+            HostBox acc = HostBox::empty();
+            uint32_t rn = 0;
+            for (int k = kBins - 1; k > 0; k--) {
+                acc.grow(bb[k]);
+                rn += cnt[k];
+                right[k] = acc.area() * (float)rn;
+            }
+            acc = HostBox::empty();
+            uint32_t ln = 0;
+            float best = __builtin_huge_valf();
+            int cut = kBins / 2;
+            for (int k = 1; k < kBins; k++) {
+                acc.grow(bb[k - 1]);
+                ln += cnt[k - 1];
+                if (ln == 0 || ln == e - b) continue;
+                const float cost = acc.area() * (float)ln + right[k];
+                if (cost < best) {
+                    best = cost;
+                    cut = k;
+                }
+            }
+            const auto mid = std::stable_partition(ids.begin() + b, ids.begin() + e,
+                                                   [&](uint32_t id) { return bin_of(id) < cut; });
+            const uint32_t m = (uint32_t)(mid - ids.begin());
+            if (m > b && m < e) return m;
+        }
+    }
     std::stable_sort(ids.begin() + b, ids.begin() + e, [&](uint32_t x, uint32_t y) {
         return boxes[x].lo[axis] + boxes[x].hi[axis] < boxes[y].lo[axis] + boxes[y].hi[axis];
     });
@@ -179,9 +289,11 @@ uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std
 }
 
 // 4-wide TLAS node over ids[b, e) (two levels of binary SAH splits); returns its link.
+// links == nullptr: leaves are instances (object mode); else leaves are the entry
+// links themselves (world mode: nodes of the world BLAS copies, or records)
 int build_tlas_node(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std::vector<HostBox> &boxes,
-                    std::vector<Bvh4Node> &nodes, uint32_t level, uint32_t &depth) {
-    if (e - b == 1) return make_leaf(ids[b], 1u);
+                    std::vector<Bvh4Node> &nodes, uint32_t level, uint32_t &depth, const std::vector<int> *links = nullptr) {
+    if (e - b == 1) return links ? (*links)[ids[b]] : make_leaf(ids[b], 1u);
     depth = std::max(depth, level + 1);
     uint32_t ranges[4][2];
     int nk = 0;
@@ -212,7 +324,7 @@ int build_tlas_node(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const st
             clo[a][k] = cb.lo[a];
             chi[a][k] = cb.hi[a];
         }
-        link[k] = build_tlas_node(ids, ranges[k][0], ranges[k][1], boxes, nodes, level + 1, depth);
+        link[k] = build_tlas_node(ids, ranges[k][0], ranges[k][1], boxes, nodes, level + 1, depth, links);
     }
     nodes[self] = encode_bvh4(nb.lo, nb.hi, clo, chi, link, nk);
     return (int)self;
@@ -226,6 +338,7 @@ int build_tlas_node(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const st
 // norms, so an object-space BLAS box never culls a triangle the world-space
 // test reports.
 void instance_margin(DevInstance &d, float vmax) {
+    d.vmax = vmax;
     float anorm = 0.f, at = 0.f, mnorm = 0.f, mt = 0.f;
     for (int r = 0; r < 3; r++) {
         anorm = std::max(anorm, std::fabs(d.to_object[4 * r]) + std::fabs(d.to_object[4 * r + 1]) +
@@ -240,7 +353,64 @@ void instance_margin(DevInstance &d, float vmax) {
     d.margin[1] = c * (anorm * (mnorm * vmax + mt) + at);
 }
 
+// World mode: the TLAS entries of instance `id` -- its world BLAS root expanded
+// `braid` levels down (partial re-braiding, Benthin et al. 2017), each with its
+// world box decoded from the quantised parent (or the instance box at the root).
+// The copy's top nodes come first in breadth-first order, so one download covers them.
+bool world_entries(TwoLevelAccel &acc, const DevInstance &d, uint32_t id, uint32_t sphere_rec, hipStream_t s) {
+    auto &out = acc.entries[id];
+    out.clear();
+    const std::array<float, 6> ibox = {d.wlo[0], d.wlo[1], d.wlo[2], d.whi[0], d.whi[1], d.whi[2]};
+    if (d.kind == PUPIL_SHAPE_SPHERE) {
+        out.push_back({make_leaf(sphere_rec, 1u), ibox});
+        return true;
+    }
+    if (d.blas_root == kTraverseDone) return true;
+    const int root = d.blas_root >= 0 ? (int)(d.blas_root - (int)d.obj_nbase + (int)d.wnode_base)
+                                      : make_leaf((uint32_t)((int64_t)leaf_first(d.blas_root) + d.wrec_delta),
+                                                  leaf_count(d.blas_root));
+    out.push_back({root, ibox});
+    uint32_t levels_nodes = 0, width = 1;
+    for (uint32_t l = 0; l < acc.braid; l++, width *= 4) levels_nodes += width;
+    const uint32_t ntop = std::min(d.obj_ncount, levels_nodes);
+    std::vector<Bvh4Node> top(ntop);
+    if (ntop && (hipMemcpyAsync(top.data(), acc.wnodes + d.wnode_base, sizeof(Bvh4Node) * ntop, hipMemcpyDeviceToHost,
+                                s) != hipSuccess ||
+                 hipStreamSynchronize(s) != hipSuccess))
+        return false;
+    for (uint32_t l = 0; l < acc.braid; l++) {
+        std::vector<std::pair<int, std::array<float, 6>>> next;
+        for (const auto &e : out) {
+            const int j = e.first - (int)d.wnode_base;
+            if (e.first < 0 || j < 0 || j >= (int)ntop) {
+                next.push_back(e);
+                continue;
+            }
+            const Bvh4Node &n = top[(size_t)j];
+            const float sc3[3] = {qfloat((n.exps & 0xFFu) << 23), qfloat(((n.exps >> 8) & 0xFFu) << 23),
+                                  qfloat(((n.exps >> 16) & 0xFFu) << 23)};
+            const float org[3] = {n.ox, n.oy, n.oz};
+            const uint32_t qlo[3] = {n.qlo_x, n.qlo_y, n.qlo_z}, qhi[3] = {n.qhi_x, n.qhi_y, n.qhi_z};
+            for (int k = 0; k < 4; k++) {
+                if (n.child[k] == kEmptyLink) continue;
+                std::array<float, 6> b;
+                for (int a = 0; a < 3; a++) {
+                    b[a] = qdecode(org[a], (qlo[a] >> (8 * k)) & 0xFFu, sc3[a]);
+                    b[3 + a] = qdecode(org[a], (qhi[a] >> (8 * k)) & 0xFFu, sc3[a]);
+                }
+                next.push_back({n.child[k], b});
+            }
+        }
+        out.swap(next);
+    }
+    return true;
+}
+
 }  // namespace
+
+void refresh_instance_margins(DevInstance &d) {
+    if (d.kind != PUPIL_SHAPE_SPHERE) instance_margin(d, d.vmax);
+}
 
 int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstance *d_insts,
                  const std::vector<uint32_t> &changed, hipStream_t s) {
@@ -254,6 +424,18 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
         if (acc.wprims)  // the changed instances' world-space triangle records
             hipLaunchKernelGGL(k_world_records, dim3(256, (uint32_t)changed.size()), dim3(kBlock), 0, s, d_insts,
                                acc.d_list, acc.d_faces, acc.prims, acc.wprims);
+        if (acc.world)  // ... and their world BLAS copies, refitted level by level from the deepest
+            for (size_t c = 0; c < changed.size(); c++) {
+                const uint32_t id = changed[c];
+                if (insts[id].kind == PUPIL_SHAPE_SPHERE || insts[id].obj_ncount == 0) continue;
+                const std::vector<uint32_t> &ls = acc.shape_levels[acc.inst_shape[id]];
+                for (size_t L = ls.size() - 1; L-- > 0;) {
+                    const uint32_t lo = ls[L], hi = ls[L + 1];
+                    const uint32_t g = std::min(1024u, (hi - lo + kBlock - 1) / kBlock);
+                    hipLaunchKernelGGL(k_world_refit, dim3(std::max(1u, g)), dim3(kBlock), 0, s, d_insts,
+                                       acc.d_list + c, lo, hi, acc.nodes4, acc.wprims, acc.wnodes, acc.d_wbox);
+                }
+            }
         std::vector<float> h(6 * (size_t)n);
         if (hipMemcpyAsync(h.data(), acc.d_boxes, sizeof(float) * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
@@ -266,6 +448,43 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
             if (hipMemcpyAsync(d_insts + id, &insts[id], sizeof(DevInstance), hipMemcpyHostToDevice, s) != hipSuccess)
                 return -1;
         }
+    }
+    if (acc.world) {  // TLAS over the braided entries of every instance
+        uint32_t srec = acc.num_wprims;  // sphere records follow the mesh records, in instance order
+        std::vector<uint32_t> sphere_rec(n, 0);
+        for (uint32_t i = 0; i < n; i++)
+            if (insts[i].kind == PUPIL_SHAPE_SPHERE) sphere_rec[i] = srec++;
+        for (uint32_t id : changed)
+            if (!world_entries(acc, insts[id], id, sphere_rec[id], s)) return -1;
+        std::vector<HostBox> eb;
+        std::vector<int> links;
+        for (uint32_t i = 0; i < n; i++)
+            for (const auto &e : acc.entries[i]) {
+                HostBox b;
+                for (int a = 0; a < 3; a++) {
+                    b.lo[a] = e.second[a];
+                    b.hi[a] = e.second[3 + a];
+                }
+                eb.push_back(b);
+                links.push_back(e.first);
+            }
+        std::vector<uint32_t> ids(eb.size());
+        std::iota(ids.begin(), ids.end(), 0u);
+        std::vector<Bvh4Node> nodes;
+        uint32_t depth = 0;
+        int root = kTraverseDone;
+        if (ids.size() == 1) root = links[0];
+        else if (!ids.empty()) root = build_tlas_node(ids, 0, (uint32_t)ids.size(), eb, nodes, 0u, depth, &links);
+        if (nodes.size() > acc.tlas_cap) return -1;
+        if (3u * depth + 3u * acc.blas_depth > (uint32_t)kTraceStackEntries) return -3;
+        acc.tlas_depth = depth;
+        if (!nodes.empty() &&
+            hipMemcpyAsync(acc.wnodes, nodes.data(), sizeof(Bvh4Node) * nodes.size(), hipMemcpyHostToDevice, s) !=
+                hipSuccess)
+            return -1;
+        acc.tlas_nodes = (uint32_t)nodes.size();
+        acc.root_link4 = (uint32_t)root;
+        return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
     }
     std::vector<HostBox> boxes(n);
     for (uint32_t i = 0; i < n; i++)
@@ -299,6 +518,11 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     const auto t0 = std::chrono::steady_clock::now();
     acc = TwoLevelAccel{};
     const uint32_t n = (uint32_t)insts.size();
+    const char *mode = std::getenv("PUPIL_TL_MODE");  // world (default) | object (A/B)
+    acc.world = !(mode && std::strcmp(mode, "object") == 0);
+    // braid 5 = TLAS over the nodes 5 levels below each instance root (config 5, r02: braid 0 / 3 / 4 / 5 / 6 ->
+    // 1557 / 1766 / 1918 / 2026 / 2052 Mrays/s vs 2205 flattened; deeper only lengthens the TLAS build)
+    if (const char *b = std::getenv("PUPIL_TL_BRAID")) acc.braid = (uint32_t)std::min(6, std::max(0, std::atoi(b)));
     // BLAS per mesh shape that some instance uses
     std::vector<uint8_t> used(shapes.size(), 0);
     std::vector<uint32_t> shape_of(n);
@@ -348,6 +572,7 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         }
         node_base[k] = total_nodes;
         prim_base[k] = total_prims;
+        if (blas[k].level_start.size() < 2) acc.world = false;  // no level order (A/B node layouts): object mode
         total_nodes += blas[k].num_nodes4;
         total_prims += sh.num_faces;
     }
@@ -390,7 +615,13 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     // per instance: BLAS root / record base / margin / world-record base, then the
     // world records, the world boxes and the TLAS
     std::vector<uint32_t> verts(n, 0), faces(n, 0), all(n);
-    uint64_t wbase = 0;
+    uint64_t wbase = 0, spheres = 0;
+    for (uint32_t i = 0; i < n; i++) spheres += insts[i].kind == PUPIL_SHAPE_SPHERE ? 1u : 0u;
+    // world mode: the TLAS (at most one node per entry, <= 4^braid entries per instance) first
+    uint32_t width = 1;
+    for (uint32_t l = 0; l < acc.braid; l++) width *= 4;
+    acc.tlas_cap = acc.world ? std::max(1u, n * width) : acc.tlas_cap;
+    uint64_t wnodes = acc.tlas_cap;
     for (uint32_t i = 0; i < n; i++) {
         all[i] = i;
         DevInstance &d = insts[i];
@@ -406,6 +637,10 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         d.attr_base = prim_base[k];
         d.wrec_delta = (int32_t)((int64_t)wbase - (int64_t)prim_base[k]);
         wbase += shapes[k].num_faces;
+        d.obj_nbase = node_base[k];
+        d.obj_ncount = blas[k].num_nodes4;
+        d.wnode_base = (uint32_t)wnodes;
+        wnodes += blas[k].num_nodes4;
         verts[i] = shapes[k].num_vertices;
         faces[i] = shapes[k].num_faces;
         instance_margin(d, shapes[k].vmax);
@@ -419,6 +654,35 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         return -1;
     }
     acc.num_wprims = (uint32_t)wbase;
+    if (acc.world) {  // world BLAS copies + sphere records appended to the world records
+        acc.entries.assign(n, {});
+        acc.inst_shape = shape_of;
+        acc.shape_levels.assign(shapes.size(), {});
+        for (size_t k = 0; k < shapes.size(); k++) acc.shape_levels[k] = blas[k].level_start;
+        std::vector<float4> sph(3 * spheres);
+        uint32_t si = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            if (insts[i].kind != PUPIL_SHAPE_SPHERE) continue;
+            sph[3 * si + 0] = make_float4(0.f, 0.f, 0.f, qfloat(insts[i].prim_offset | kPrimSphereBit));
+            sph[3 * si + 1] = make_float4(0.f, 0.f, 0.f, qfloat(i));
+            sph[3 * si + 2] = make_float4(0.f, 0.f, 0.f, qfloat(insts[i].bin));
+            si++;
+        }
+        float4 *grown = nullptr;
+        if (wnodes >= (1ull << 31) ||
+            hipMalloc((void **)&acc.wnodes, sizeof(Bvh4Node) * (size_t)wnodes) != hipSuccess ||
+            hipMalloc((void **)&acc.d_wbox, sizeof(float) * 6 * (size_t)wnodes) != hipSuccess ||
+            hipMalloc((void **)&grown, sizeof(float4) * 3 * (size_t)std::max<uint64_t>(1, wbase + spheres)) != hipSuccess ||
+            (spheres && hipMemcpy(grown + 3 * wbase, sph.data(), sizeof(float4) * sph.size(), hipMemcpyHostToDevice) !=
+                            hipSuccess)) {
+            if (grown) (void)hipFree(grown);
+            free_two_level(acc);
+            return -1;
+        }
+        (void)hipFree(acc.wprims);
+        acc.wprims = grown;
+        acc.num_wnodes = (uint32_t)wnodes;
+    }
     if (hipMemcpy(acc.d_verts, verts.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_insts, insts.data(), sizeof(DevInstance) * n, hipMemcpyHostToDevice) != hipSuccess ||
         (trc = rebuild_tlas(acc, insts, d_insts, all, s)) != 0) {
@@ -430,7 +694,8 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
 }
 
 void free_two_level(TwoLevelAccel &acc) {
-    void *p[] = {acc.nodes4, acc.prims, acc.attrs, acc.d_boxes, acc.d_list, acc.d_verts, acc.wprims, acc.d_faces};
+    void *p[] = {acc.nodes4, acc.prims, acc.attrs, acc.d_boxes, acc.d_list, acc.d_verts, acc.wprims, acc.d_faces,
+                 acc.wnodes, acc.d_wbox};
     for (void *x : p)
         if (x) (void)hipFree(x);
     acc = TwoLevelAccel{};

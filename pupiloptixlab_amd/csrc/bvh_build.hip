@@ -767,7 +767,7 @@ hipError_t dmalloc(T **p, size_t count) {
 // nodes4 must hold n - 1 entries; returns the number of 4-wide nodes.
 hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
                          const int2 *ranges, const Aabb *node_boxes, uint32_t leaf_size, Bvh4Node *nodes4,
-                         uint32_t *num_nodes4, uint32_t *depth4, hipStream_t s) {
+                         uint32_t *num_nodes4, uint32_t *depth4, std::vector<uint32_t> *level_start, hipStream_t s) {
     int *items_a = nullptr, *items_b = nullptr;
     int4 *clist = nullptr;
     unsigned long long *cnt = nullptr, *sums = nullptr, *total = nullptr;
@@ -781,9 +781,11 @@ hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_bo
     if (!err) err = dmalloc(&total, 1);
     int base = 0, items = 1;
     uint32_t levels = 0;  // breadth first: one iteration per BVH4 level
+    if (level_start) level_start->clear();
     if (!err) err = hipMemsetAsync(items_a, 0, sizeof(int), s);  // binary root 0
     const auto grid = [](int m) { return dim3((unsigned)((m + kBlock - 1) / kBlock)); };
     while (!err && items > 0) {
+        if (level_start) level_start->push_back((uint32_t)base);
         hipLaunchKernelGGL(k_collapse_pick, grid(items), dim3(kBlock), 0, s, items, items_a, children, ranges,
                            node_boxes, leaf_size, clist, cnt);
         const int nb = (items + per - 1) / per;
@@ -803,6 +805,7 @@ hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_bo
     }
     *num_nodes4 = (uint32_t)base;
     *depth4 = levels;
+    if (level_start) level_start->push_back((uint32_t)base);
     void *bufs[] = {items_a, items_b, clist, cnt, sums, total};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -967,6 +970,7 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     if (leaf_size < 1) leaf_size = 1;
     if (leaf_size > (uint32_t)kLeafMax) leaf_size = kLeafMax;
     out.depth4 = 0;
+    out.level_start.clear();
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
@@ -1041,9 +1045,12 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
                 err = dmalloc(&out.nodes4, (size_t)(n - 1));
                 if (!err)
                     err = collapse_bvh4(n, vi, boxes, children, ranges, node_boxes, leaf_size, out.nodes4,
-                                        &out.num_nodes4, &out.depth4, s);
+                                        &out.num_nodes4, &out.depth4, &out.level_start, s);
                 const char *order = std::getenv("PUPIL_NODE_ORDER");
-                if (!err && order && out.num_nodes4 > 1) err = relabel_nodes4(out.nodes4, out.num_nodes4, order, s);
+                if (!err && order && out.num_nodes4 > 1) {
+                    err = relabel_nodes4(out.nodes4, out.num_nodes4, order, s);
+                    out.level_start.clear();  // no longer breadth first
+                }
             } else if (!err) {
             // 4-wide quantized tree: depth parity -> flags -> compact indices -> nodes
             uint32_t *depth = ko, *flags4 = vo, *idx4 = nullptr;  // the sort's free ping-pong buffers

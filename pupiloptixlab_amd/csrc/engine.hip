@@ -556,8 +556,9 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         sc.two_level = 1;
         sc.nodes = nullptr;
         sc.root_link = (uint32_t)kTraverseDone;
-        sc.nodes4 = pt->tl.nodes4;
-        sc.prims = pt->tl.prims;
+        sc.tl_world = pt->tl.world ? 1u : 0u;
+        sc.nodes4 = pt->tl.world ? pt->tl.wnodes : pt->tl.nodes4;
+        sc.prims = pt->tl.world ? pt->tl.wprims : pt->tl.prims;
         sc.wprims = pt->tl.wprims;
         sc.attrs = pt->tl.attrs;
         sc.root_link4 = pt->tl.root_link4;
@@ -596,7 +597,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         return cleanup(fail(PUPIL_ERR_HIP, "workspace clear failed"));
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
-    pt->totals.bvh_nodes = pt->two_level ? pt->tl.tlas_nodes + (pt->tl.num_nodes4 - pt->tl.tlas_cap)
+    pt->totals.bvh_nodes = pt->two_level ? two_level_nodes(pt->tl)
                            : (pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes);
     pt->totals.two_level = pt->two_level ? 1u : 0u;
     pt->totals.bvh_depth = pt->two_level ? pt->tl.tlas_depth + pt->tl.blas_depth : pt->bvh.depth4;
@@ -625,6 +626,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     DevInstance &d = pt->h_insts[instance];
     std::memcpy(d.to_world, to_world, sizeof(d.to_world));
     std::memcpy(d.to_object, to_object, sizeof(d.to_object));
+    if (pt->two_level) refresh_instance_margins(d);  // they depend on the transform
     HIP_TRY(hipMemcpy(pt->d_insts + instance, &d, sizeof(DevInstance), hipMemcpyHostToDevice));
     if (pt->two_level) {  // new world box for the instance, TLAS rebuilt over all instance boxes
         const auto t0 = std::chrono::steady_clock::now();
@@ -632,7 +634,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
         if (trc == -3) return fail(PUPIL_ERR_UNSUPPORTED, "TLAS + BLAS deeper than the traversal stacks hold");
         if (trc != 0) return fail(PUPIL_ERR_HIP, "TLAS rebuild failed");
         pt->sc.root_link4 = pt->tl.root_link4;
-        pt->totals.bvh_nodes = pt->tl.tlas_nodes + (pt->tl.num_nodes4 - pt->tl.tlas_cap);
+        pt->totals.bvh_nodes = two_level_nodes(pt->tl);
         pt->totals.bvh_depth = pt->tl.tlas_depth + pt->tl.blas_depth;
         pt->totals.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         return PUPIL_OK;

@@ -2,6 +2,8 @@
 // LBVH builder (implemented in pt_kernels.hip / bvh_build.hip).
 #pragma once
 
+#include <vector>
+
 #include <hip/hip_runtime.h>
 
 #include "pt_scene.h"
@@ -151,6 +153,9 @@ struct BvhBuildOutput {
     uint32_t num_nodes;
     uint32_t num_nodes4;
     uint32_t depth4;    // levels of the BVH4 (1 = root only); 0 = not measured (A/B collapse)
+    // first node of each BVH4 level (breadth-first collapse order) and the end; empty when
+    // not measured.  Children always lie on a later level (bottom-up refits walk it backwards).
+    std::vector<uint32_t> level_start;
 };
 int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms,
                bool force_lbvh = false);

@@ -829,7 +829,10 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         if (MODE == kModeExtend || MODE == kModeMixed) {
             uint32_t bin = 0;
             if (done && !any) {
-                ps.hit[p] = make_float4(found ? tmax : -1.f, b1, b2, __uint_as_float(found ? best_idx : kMissIndex));
+                // hit index: the record (flat) or the global primitive id (two-level shading,
+                // reconstruct(); the world-mode flat kernel keeps it in best_key)
+                const uint32_t hidx = !TL && sc.two_level ? best_key : best_idx;
+                ps.hit[p] = make_float4(found ? tmax : -1.f, b1, b2, __uint_as_float(found ? hidx : kMissIndex));
                 if (found) {
                     if (TL) {
                         bin = sc.instances[sc.prim_inst[best_idx]].bin;
@@ -1329,7 +1332,7 @@ static uint32_t trace4_blocks(const DeviceScene &sc, uint32_t ovf_threads) {
         const char *e = std::getenv("PUPIL_TRACE_GRID_WAVES");
         return e ? std::max(1, std::atoi(e)) : 0;
     }();
-    const uint32_t occ = sc.two_level ? kTraceWavesPerSimdTL : kTraceWavesPerSimd;
+    const uint32_t occ = sc.two_level && !sc.tl_world ? kTraceWavesPerSimdTL : kTraceWavesPerSimd;
     const uint32_t waves = forced ? std::min(occ, (uint32_t)forced) : occ;
     const uint32_t resident = sc.num_cus * 4u * waves / (kTraceBlock / 64u);
     return std::min(ovf_threads / kTraceBlock, std::max(1u, resident));
@@ -1341,7 +1344,7 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
                           uint32_t ovf_threads, const TraceStats *stats, hipStream_t s) {
     const TraceStats st = stats ? *stats : TraceStats{nullptr};
     const uint32_t blocks = trace4_blocks(sc, ovf_threads);
-    if (sc.two_level) {
+    if (sc.two_level && !sc.tl_world) {
         if (stats)
             hipLaunchKernelGGL((k_trace4tl<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
                                ovf, ovf_threads, st);
@@ -1362,7 +1365,7 @@ void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, ui
     if (sc.bvh_width == 4 && sc.trace_refill) {  // the production kernel, fed from a ray array
         const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, sc.trace_node_min, rays, out};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
-        if (sc.two_level) {
+        if (sc.two_level && !sc.tl_world) {
             if (any)
                 hipLaunchKernelGGL((k_trace4tl<kModeRays, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
                                    PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});

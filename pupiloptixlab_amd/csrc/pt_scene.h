@@ -85,6 +85,10 @@ struct DevInstance {
     float margin[2];      // object-space box margin: margin[0] * (|o| + t |d|) + margin[1]
     float wlo[3], whi[3];  // world box of the instance's world-space primitives
     int32_t wrec_delta;    // world-space record of BLAS record i: wprims[3 * (i + wrec_delta)]
+    // world-space copy of the shape's BLAS (two-level "world" mode): object nodes
+    // [obj_nbase, obj_nbase + obj_ncount) -> world nodes from wnode_base
+    uint32_t obj_nbase, obj_ncount, wnode_base;
+    float vmax;  // largest |object-space vertex coordinate| of the shape (margins)
 };
 
 struct alignas(16) BvhNode {
@@ -141,6 +145,8 @@ struct DeviceScene {
     uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
     uint32_t num_cus;       // compute units of the device (persistent grid size)
     uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node
+    uint32_t tl_world;        // two-level "world" mode: nodes4 = braided TLAS + world-space BLAS copies,
+                              // prims = flat-format world records; traversed by the flat kernels
     uint32_t two_level;       // 1: nodes4 = TLAS over instances + object-space BLAS per shape;
                               //    prims/attrs = BLAS records, hit index = global primitive id
     const float4 *wprims;       // two-level: per-instance world-space triangle records (see accel_two_level.hip)
