@@ -352,7 +352,10 @@ def roofline(args, st_bytes, trace_ms, trace_launches):
     launches = max(1, trace_launches)
     ms = trace_ms / launches  # HIP events on the render stream, the extra timing frame
     sec = ms * 1e-3
-    nodes = st_bytes["node_visits"] / launches
+    visits = st_bytes["node_visits"] / launches
+    # lanes of a wave on the same node share one fetch: the distinct fetches per wave step are
+    # the gathers the memory system serves, the quantity the random-gather ceiling measures
+    nodes = (st_bytes.get("unique_node_fetches") or st_bytes["node_visits"]) / launches
     alg_bytes = st_bytes["trace_bytes"] / launches
     kernel = ("k_trace4 (persistent BVH4 traversal, all launches of a frame: primary extend + "
               "per-bounce extension+shadow)")
@@ -361,9 +364,12 @@ def roofline(args, st_bytes, trace_ms, trace_launches):
     if ceil and sec > 0:
         cands["node-gather"] = {"achieved": nodes / sec / 1e9, "peak": ceil["ceiling_gnodes_per_s"],
                                 "unit": "Gnode/s",
-                                "how": "node visits per launch (instrumented frame) / HIP-event launch time; peak = "
-                                       f"build/ubench_gather dependent 64-B gathers, {ceil['table_mb']:.0f} MB table, "
-                                       "best waves/SIMD, measured in this run",
+                                "how": "distinct node fetches per wave step, per launch (counter frame) / HIP-event "
+                                       "launch time; peak = build/ubench_gather dependent random 64-B gathers, "
+                                       f"{ceil['table_mb']:.0f} MB table (the BVH's size), best waves/SIMD, measured in "
+                                       "this run",
+                                "node_visits_per_launch": round(visits, 1),
+                                "distinct_fetches_per_launch": round(nodes, 1),
                                 "ceiling_per_waves_per_simd": ceil.get("per_waves_per_simd")}
     pmc = pmc_record(args)
     traffic = None

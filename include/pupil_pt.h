@@ -241,6 +241,10 @@ typedef struct pupil_pt_counters {
      * create, trees needing more than the traversal stacks hold are rebuilt with the
      * Karras LBVH or rejected with PUPIL_ERR_UNSUPPORTED */
     uint64_t bvh_depth;
+    /* collect_stats: node fetches counted once per distinct node per wave step (the
+     * lanes of a wave on the same node share one fetch) -- the gather rate the memory
+     * system serves, comparable with independent random gathers */
+    uint64_t unique_node_fetches;
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;

@@ -41,6 +41,7 @@ struct TwoLevelAccel {
     uint32_t num_wnodes = 0;
     std::vector<std::vector<std::pair<int, std::array<float, 6>>>> entries;  // per instance: TLAS entries
     std::vector<uint32_t> inst_shape;                  // shape of each instance (0xFFFFFFFF: sphere)
+    std::vector<Bvh4Node> tlas_host;                   // host copy of the world-mode TLAS (refits)
     std::vector<std::vector<uint32_t>> shape_levels;   // per shape: BVH4 level starts of its BLAS (+ end)
     uint32_t root_link4 = (uint32_t)kTraverseDone;
     double build_ms = 0.0;
@@ -62,8 +63,9 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
 // Recomputes the world boxes of the `changed` instances (transforms already in
 // insts / d_insts) and rebuilds the TLAS.  -3: the TLAS + BLAS depth exceeds the
 // traversal stacks (kTraceStackEntries).
+// refit (world mode): keep the TLAS topology and refit its boxes instead of rebuilding.
 int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstance *d_insts,
-                 const std::vector<uint32_t> &changed, hipStream_t s);
+                 const std::vector<uint32_t> &changed, hipStream_t s, bool refit = false);
 void free_two_level(TwoLevelAccel &acc);
 // BLAS box margins of an instance after its transform changed (uses its stored vmax)
 void refresh_instance_margins(DevInstance &d);

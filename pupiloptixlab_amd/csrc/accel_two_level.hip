@@ -24,6 +24,7 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <unordered_map>
 #include <vector>
 
 #include "accel_two_level.h"
@@ -412,8 +413,51 @@ void refresh_instance_margins(DevInstance &d) {
     if (d.kind != PUPIL_SHAPE_SPHERE) instance_margin(d, d.vmax);
 }
 
+// World mode, RenderInstanceUpdate: the TLAS keeps its topology and its boxes are
+// refitted bottom up to the changed entries (the reference refits its IAS,
+// ias_manager.cpp:116-151).  TLAS nodes are numbered parent first, so walking them
+// backwards sees every child before its parent.
+bool refit_world_tlas(TwoLevelAccel &acc, uint32_t n, hipStream_t s) {
+    if (acc.tlas_host.size() != acc.tlas_nodes || acc.tlas_nodes == 0) return false;
+    std::unordered_map<int, std::array<float, 6>> eb;
+    for (uint32_t i = 0; i < n; i++)
+        for (const auto &e : acc.entries[i]) eb[e.first] = e.second;
+    std::vector<std::array<float, 6>> nb(acc.tlas_nodes);
+    for (uint32_t v = acc.tlas_nodes; v-- > 0;) {
+        Bvh4Node &nd = acc.tlas_host[v];
+        float clo[3][4], chi[3][4], nlo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()},
+                                    nhi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+        int link[4];
+        int nk = 0;
+        for (int k = 0; k < 4; k++) {
+            const int l = nd.child[k];
+            if (l == kEmptyLink) continue;
+            std::array<float, 6> b;
+            if (l >= 0 && (uint32_t)l < acc.tlas_nodes) {
+                b = nb[(size_t)l];
+            } else {
+                auto it = eb.find(l);
+                if (it == eb.end()) return false;
+                b = it->second;
+            }
+            for (int a = 0; a < 3; a++) {
+                clo[a][nk] = b[a];
+                chi[a][nk] = b[3 + a];
+                nlo[a] = std::min(nlo[a], b[a]);
+                nhi[a] = std::max(nhi[a], b[3 + a]);
+            }
+            link[nk++] = l;
+        }
+        nd = encode_bvh4(nlo, nhi, clo, chi, link, nk);
+        nb[v] = {nlo[0], nlo[1], nlo[2], nhi[0], nhi[1], nhi[2]};
+    }
+    return hipMemcpyAsync(acc.wnodes, acc.tlas_host.data(), sizeof(Bvh4Node) * acc.tlas_nodes, hipMemcpyHostToDevice,
+                          s) == hipSuccess &&
+           hipStreamSynchronize(s) == hipSuccess;
+}
+
 int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstance *d_insts,
-                 const std::vector<uint32_t> &changed, hipStream_t s) {
+                 const std::vector<uint32_t> &changed, hipStream_t s, bool refit) {
     const uint32_t n = (uint32_t)insts.size();
     if (!changed.empty()) {
         if (hipMemcpyAsync(acc.d_list, changed.data(), sizeof(uint32_t) * changed.size(), hipMemcpyHostToDevice, s) !=
@@ -456,6 +500,7 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
             if (insts[i].kind == PUPIL_SHAPE_SPHERE) sphere_rec[i] = srec++;
         for (uint32_t id : changed)
             if (!world_entries(acc, insts[id], id, sphere_rec[id], s)) return -1;
+        if (refit && refit_world_tlas(acc, n, s)) return 0;
         std::vector<HostBox> eb;
         std::vector<int> links;
         for (uint32_t i = 0; i < n; i++)
@@ -483,6 +528,7 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
                 hipSuccess)
             return -1;
         acc.tlas_nodes = (uint32_t)nodes.size();
+        acc.tlas_host = nodes;
         acc.root_link4 = (uint32_t)root;
         return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
     }

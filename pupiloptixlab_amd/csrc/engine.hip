@@ -630,7 +630,10 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     HIP_TRY(hipMemcpy(pt->d_insts + instance, &d, sizeof(DevInstance), hipMemcpyHostToDevice));
     if (pt->two_level) {  // new world box for the instance, TLAS rebuilt over all instance boxes
         const auto t0 = std::chrono::steady_clock::now();
-        const int trc = rebuild_tlas(pt->tl, pt->h_insts, pt->d_insts, {instance}, pt->own_stream);
+        // world mode refits the TLAS like the reference's IAS update (PUPIL_TL_UPDATE=rebuild: full build)
+        const char *um = std::getenv("PUPIL_TL_UPDATE");
+        const bool refit = !(um && std::strcmp(um, "rebuild") == 0);
+        const int trc = rebuild_tlas(pt->tl, pt->h_insts, pt->d_insts, {instance}, pt->own_stream, refit);
         if (trc == -3) return fail(PUPIL_ERR_UNSUPPORTED, "TLAS + BLAS deeper than the traversal stacks hold");
         if (trc != 0) return fail(PUPIL_ERR_HIP, "TLAS rebuild failed");
         pt->sc.root_link4 = pt->tl.root_link4;
@@ -898,6 +901,7 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
             c.node_visits = tc[0] + tc[14];
             c.prim_tests = tc[1] + tc[15];
             c.shadow_rays_reference = tc[16];
+            c.unique_node_fetches = tc[18];
             c.extend_node_visits = tc[0];
             c.extend_prim_tests = tc[1];
             const double rays = (double)(c.primary_rays + c.extension_rays + c.shadow_rays);

@@ -102,7 +102,8 @@ struct FrameParams {
 };
 
 struct TraceStats {
-    unsigned long long *counters;  // [0..1] closest-hit nodes/prims, [14..15] shadow, [2..13] diagnostics
+    unsigned long long *counters;  // [0..1] closest-hit nodes/prims, [14..15] shadow, [2..13] diagnostics,
+                                   // [16] reference shadow rays, [18] distinct node fetches
     // PUPIL_TRACE_TAIL diagnostics (STATS kernels only, else null): per wave of the
     // persistent launch, s_memrealtime (100 MHz) at start, when its dequeue found
     // the work list drained, at exit, and the rays it took

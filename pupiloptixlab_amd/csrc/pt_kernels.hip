@@ -609,6 +609,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     st.ovf_stride = ovf_threads;
     st.reset();
     uint32_t nv = 0, npt = 0, nv_sh = 0, npt_sh = 0;  // mixed: shadow-ray counts apart
+    uint32_t n_unique = 0;  // STATS: distinct node fetches (per wave step)
     // STATS-only SIMD-efficiency diagnostics, each event counted by one lane:
     // node-loop wave iterations / active lanes, leaf-loop iterations / active
     // lanes, refills / lanes refilled
@@ -738,6 +739,14 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         dg[0]++;
                         dg[1] += (unsigned long long)__popcll(m);
                     }
+                    // distinct nodes fetched by this wave step (lanes of a wave on the same node
+                    // share one fetch): the gather rate the memory system actually serves
+                    bool dup = false;
+                    for (int j = 0; j < 64; j++) {
+                        const int nj = __shfl(node, j);
+                        if (j < (int)lane_id() && ((m >> j) & 1ull) && nj == node) dup = true;
+                    }
+                    n_unique += dup ? 0u : 1u;
                 }
                 float t[4];
                 int l[4];
@@ -864,6 +873,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     }
     flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
     if (MODE == kModeMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
+    flush_stats<STATS>(&stats, n_unique, 0u, 18);
     if (STATS && stats.wave_times && lane_id() == 0) {
         unsigned long long *w = stats.wave_times + 4ull * (blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u);
         w[0] = t_start;

@@ -14,7 +14,7 @@ def test_roofline_normalises_per_launch_and_picks_the_binding_ceiling(monkeypatc
         config = 4
 
     # config 4, r02: 1.80 G node visits per frame over 4 traversal launches, 15.6 ms of traversal
-    st = {"node_visits": 1.80e9, "trace_bytes": 143.3e9, "bvh_nodes": 267580}
+    st = {"node_visits": 1.80e9, "unique_node_fetches": 1.80e9, "trace_bytes": 143.3e9, "bvh_nodes": 267580}
     r = bench.roofline(A, st, trace_ms=15.64, trace_launches=4)
     assert abs(r["ms_per_launch"] - 3.91) < 1e-9
     c = r["ceilings"]
