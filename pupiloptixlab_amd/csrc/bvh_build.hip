@@ -1130,4 +1130,123 @@ int build_bvh_bounded(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t lea
     return 0;
 }
 
+// ------------------------------------------------------------------ refit (RenderInstanceUpdate)
+namespace {
+
+// Records of the moved instance (b.w = instance) get its new world vertices, written
+// exactly as k_prim_setup writes them (global id in a.w: sphere bit + id).
+__global__ void k_refit_records(BvhBuildInput in, uint32_t n, float4 *recs, uint32_t moved) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    if (__float_as_uint(recs[3 * r + 1].w) != moved) return;
+    const uint32_t gid = __float_as_uint(recs[3 * r].w) & ~kPrimSphereBit;
+    const DevInstance &inst = in.instances[moved];
+    if (inst.kind == PUPIL_SHAPE_SPHERE) {
+        const float *m = inst.to_world;
+        const vec3 c = v3(m[3], m[7], m[11]);
+        const float ex = sqrtf(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.001f;
+        const float ey = sqrtf(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.001f;
+        const float ez = sqrtf(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.001f;
+        recs[3 * r + 0] = make_float4(c.x, c.y, c.z, recs[3 * r].w);
+        recs[3 * r + 1] = make_float4(ex, ey, ez, recs[3 * r + 1].w);
+        return;
+    }
+    const uint32_t local = gid - inst.prim_offset;
+    const uint32_t i0 = inst.indices[3 * local], i1 = inst.indices[3 * local + 1], i2 = inst.indices[3 * local + 2];
+    const float *P = inst.positions;
+    const vec3 w0 = xform_point(inst.to_world, v3(P[3 * i0], P[3 * i0 + 1], P[3 * i0 + 2]));
+    const vec3 w1 = xform_point(inst.to_world, v3(P[3 * i1], P[3 * i1 + 1], P[3 * i1 + 2]));
+    const vec3 w2 = xform_point(inst.to_world, v3(P[3 * i2], P[3 * i2 + 1], P[3 * i2 + 2]));
+    recs[3 * r + 0] = make_float4(w0.x, w0.y, w0.z, recs[3 * r].w);
+    recs[3 * r + 1] = make_float4(w1.x, w1.y, w1.z, recs[3 * r + 1].w);
+    recs[3 * r + 2] = make_float4(w2.x, w2.y, w2.z, recs[3 * r + 2].w);
+}
+
+// One BVH4 level, bottom up: child boxes from the records under a leaf (exact; a
+// sphere's padded box) or from the child's box of the previous launch; re-quantised.
+__global__ void k_refit_level(Bvh4Node *nodes, uint32_t lo, uint32_t hi, const float4 *recs, float *nbox) {
+    for (uint32_t j = lo + blockIdx.x * blockDim.x + threadIdx.x; j < hi; j += gridDim.x * blockDim.x) {
+        const Bvh4Node n = nodes[j];
+        float clo[3][4], chi[3][4];
+        float nlo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+        float nhi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+        int link[4];
+        int nk = 0;
+        for (int k = 0; k < 4; k++) {
+            const int l = n.child[k];
+            if (l == kEmptyLink) continue;
+            float bl[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+            float bh[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+            if (l >= 0) {
+                for (int a = 0; a < 3; a++) {
+                    bl[a] = nbox[6 * (size_t)l + a];
+                    bh[a] = nbox[6 * (size_t)l + 3 + a];
+                }
+            } else {
+                for (uint32_t r = leaf_first(l); r < leaf_first(l) + leaf_count(l); r++) {
+                    const float4 a = recs[3 * r], b = recs[3 * r + 1], c = recs[3 * r + 2];
+                    if (__float_as_uint(a.w) & kPrimSphereBit) {
+                        bl[0] = fminf(bl[0], a.x - b.x);
+                        bl[1] = fminf(bl[1], a.y - b.y);
+                        bl[2] = fminf(bl[2], a.z - b.z);
+                        bh[0] = fmaxf(bh[0], a.x + b.x);
+                        bh[1] = fmaxf(bh[1], a.y + b.y);
+                        bh[2] = fmaxf(bh[2], a.z + b.z);
+                    } else {
+                        bl[0] = fminf(bl[0], fminf(fminf(a.x, b.x), c.x));
+                        bl[1] = fminf(bl[1], fminf(fminf(a.y, b.y), c.y));
+                        bl[2] = fminf(bl[2], fminf(fminf(a.z, b.z), c.z));
+                        bh[0] = fmaxf(bh[0], fmaxf(fmaxf(a.x, b.x), c.x));
+                        bh[1] = fmaxf(bh[1], fmaxf(fmaxf(a.y, b.y), c.y));
+                        bh[2] = fmaxf(bh[2], fmaxf(fmaxf(a.z, b.z), c.z));
+                    }
+                }
+            }
+            for (int a = 0; a < 3; a++) {
+                clo[a][nk] = bl[a];
+                chi[a][nk] = bh[a];
+                nlo[a] = fminf(nlo[a], bl[a]);
+                nhi[a] = fmaxf(nhi[a], bh[a]);
+            }
+            link[nk++] = l;
+        }
+        nodes[j] = encode_bvh4(nlo, nhi, clo, chi, link, nk);
+        for (int a = 0; a < 3; a++) {
+            nbox[6 * (size_t)j + a] = nlo[a];
+            nbox[6 * (size_t)j + 3 + a] = nhi[a];
+        }
+    }
+}
+
+}  // namespace
+
+int refit_bvh4(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t moved, hipStream_t s, double *ms) {
+    if (out.level_start.size() < 2 || !out.nodes4 || out.num_nodes4 == 0) return -1;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, s);
+    float *nbox = nullptr;
+    hipError_t err = dmalloc(&nbox, 6 * (size_t)out.num_nodes4);
+    if (!err) {
+        const uint32_t n = in.num_prims;
+        hipLaunchKernelGGL(k_refit_records, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, in, n, out.prims, moved);
+        for (size_t L = out.level_start.size() - 1; L-- > 0;) {
+            const uint32_t lo = out.level_start[L], hi = out.level_start[L + 1];
+            const uint32_t g = std::max(1u, std::min(4096u, (hi - lo + kBlock - 1) / kBlock));
+            hipLaunchKernelGGL(k_refit_level, dim3(g), dim3(kBlock), 0, s, out.nodes4, lo, hi, out.prims, nbox);
+        }
+        err = hipGetLastError();
+    }
+    (void)hipEventRecord(e1, s);
+    if (!err) err = hipEventSynchronize(e1);
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, e0, e1);
+    if (ms) *ms = t;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (nbox) (void)hipFree(nbox);
+    return err == hipSuccess ? 0 : -2;
+}
+
 }  // namespace pupil

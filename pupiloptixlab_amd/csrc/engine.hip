@@ -643,6 +643,15 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
         return PUPIL_OK;
     }
     BvhBuildInput bin{pt->num_prims, pt->d_prim_inst, pt->d_insts, pt->d_mats};
+    // refit in place (PUPIL_FLAT_UPDATE=rebuild, or the BVH2 A/B node format: full rebuild)
+    const char *fu = std::getenv("PUPIL_FLAT_UPDATE");
+    if (pt->sc.bvh_width == 4 && !(fu && std::strcmp(fu, "rebuild") == 0)) {
+        double rms = 0.0;
+        if (refit_bvh4(bin, pt->bvh, instance, pt->own_stream, &rms) == 0) {
+            pt->totals.build_ms = rms;
+            return PUPIL_OK;
+        }
+    }
     BvhBuildOutput nb{};
     double ms = 0.0;
     const int brc = build_bvh_bounded(bin, nb, pt->leaf_size, pt->own_stream, &ms, 0);

@@ -166,5 +166,9 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
 int build_bvh_bounded(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s,
                       double *build_ms, uint32_t reserve);
 void free_lbvh(BvhBuildOutput &out);
+// RenderInstanceUpdate without a rebuild: the records of instance `moved` get its new
+// world vertices and every BVH4 node box is refitted bottom up (topology kept, like the
+// reference's IAS update).  Needs the breadth-first level order; -1 when unavailable.
+int refit_bvh4(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t moved, hipStream_t s, double *ms);
 
 }  // namespace pupil
