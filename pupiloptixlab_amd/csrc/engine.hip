@@ -500,10 +500,11 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     pt->leaf_size = 2u;  // with the 7-wave traversal: 2 beats 3 by 2 %, 1 and 4 are slower (config 4)
     if (const char *ls = std::getenv("PUPIL_LEAF_SIZE")) pt->leaf_size = (uint32_t)std::min(8, std::max(1, std::atoi(ls)));
     // Acceleration structure (replaces the GAS + IAS builds): one flattened BVH over
-    // world-space primitives (default: on config 5 it traces 3.2x faster than the
-    // two-level structure), or a TLAS over per-shape object-space BLASes
-    // (PUPIL_ACCEL=two_level; automatic when the flattened primitive count would pass
-    // the flat build's 2^28 limit).  Both give bit-identical hits.
+    // world-space primitives (default: on config 5 it traces 1.08x faster than the
+    // two-level world mode), or a TLAS over per-instance BLASes (PUPIL_ACCEL=two_level,
+    // which bench.py selects for config 5: cheaper instance updates; automatic when
+    // the flattened primitive count would pass the flat build's 2^28 limit).  Both
+    // give bit-identical hits.
     {
         std::vector<uint32_t> uses(scene->num_shapes, 0), inst_shape(scene->num_instances);
         uint64_t flat_prims = 0;
