@@ -35,9 +35,11 @@ PT_HD float qfloat(uint32_t u) {
 // decode used by the traversal: origin + (float)q * scale (q*scale is exact)
 PT_HD float qdecode(float origin, uint32_t q, float scale) { return origin + (float)q * scale; }
 
-// Up to 4 child intervals [clo[k], chi[k]] (k < nk) inside [lo, hi] on one axis.
-PT_HD void quantize_axis(float lo, float hi, const float *clo, const float *chi, int nk, float &origin,
-                         uint32_t &ebyte, uint32_t &qlo, uint32_t &qhi) {
+// Up to N (4 or 8) child intervals [clo[k], chi[k]] (k < nk) inside [lo, hi] on
+// one axis; byte k % 4 of word k / 4 of qlo / qhi holds child k's plane.
+template <int N>
+PT_HD void quantize_axis_n(float lo, float hi, const float *clo, const float *chi, int nk, float &origin,
+                           uint32_t &ebyte, uint32_t *qlo, uint32_t *qhi) {
     origin = lo;
     const float ext = hi - lo;
     float scale;
@@ -49,9 +51,8 @@ PT_HD void quantize_axis(float lo, float hi, const float *clo, const float *chi,
     }
     for (int attempt = 0; attempt < 8; attempt++) {
         bool ok = true;
-        qlo = 0u;
-        qhi = 0u;
-        for (int k = 0; k < 4; k++) {
+        for (int w = 0; w < N / 4; w++) qlo[w] = qhi[w] = 0u;
+        for (int k = 0; k < N; k++) {
             uint32_t a = 255u, b = 0u;  // empty slot: lo > hi
             if (k < nk) {
                 float fa = floorf((clo[k] - origin) / scale);
@@ -64,13 +65,18 @@ PT_HD void quantize_axis(float lo, float hi, const float *clo, const float *chi,
                 while (b < 255u && qdecode(origin, b, scale) < chi[k]) b++;
                 if (qdecode(origin, a, scale) > clo[k] || qdecode(origin, b, scale) < chi[k]) ok = false;
             }
-            qlo |= a << (8 * k);
-            qhi |= b << (8 * k);
+            qlo[k >> 2] |= a << (8 * (k & 3));
+            qhi[k >> 2] |= b << (8 * (k & 3));
         }
         if (ok) break;
         scale = scale * 2.f;
     }
     ebyte = (qbits(scale) >> 23) & 0xFFu;
+}
+
+PT_HD void quantize_axis(float lo, float hi, const float *clo, const float *chi, int nk, float &origin,
+                         uint32_t &ebyte, uint32_t &qlo, uint32_t &qhi) {
+    quantize_axis_n<4>(lo, hi, clo, chi, nk, origin, ebyte, &qlo, &qhi);
 }
 
 // One BVH4 node from its box, nk <= 4 child boxes and links.

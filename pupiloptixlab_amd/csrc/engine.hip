@@ -89,6 +89,7 @@ struct pupil_pt {
     std::vector<void *> allocs;
     BvhBuildOutput bvh{};
     bool two_level = false;  // TLAS + per-shape BLAS (accel_two_level.hip) instead of one flattened BVH
+    uint32_t bvh_width = 4;  // flattened BVH node format (PUPIL_BVH_WIDTH)
     TwoLevelAccel tl{};
     uint32_t width = 0, height = 0, max_depth = 1;
     uint32_t num_prims = 0;
@@ -544,6 +545,9 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
             pt->build_ms = pt->tl.build_ms;
         } else {
             BvhBuildInput bin{pt->num_prims, d_prim_inst, d_insts, d_mats};
+            if (const char *w = std::getenv("PUPIL_BVH_WIDTH"))  // node format: 4 (default), 8, or 2 (A/B)
+                pt->bvh_width = (uint32_t)std::atoi(w) == 8 ? 8u : ((uint32_t)std::atoi(w) == 2 ? 2u : 4u);
+            bin.wide8 = pt->bvh_width == 8 ? 1u : 0u;
             const int brc = build_bvh_bounded(bin, pt->bvh, pt->leaf_size, pt->own_stream, &pt->build_ms, 0);
             if (brc == -3) return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "BVH deeper than the traversal stacks hold"));
             if (brc != 0) return cleanup(fail(PUPIL_ERR_HIP, "LBVH build failed"));
@@ -570,15 +574,16 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         sc.root_link = pt->bvh.root_link;
         sc.nodes4 = pt->bvh.nodes4;
         sc.root_link4 = pt->bvh.root_link4;
-        if (const char *w = std::getenv("PUPIL_BVH_WIDTH"))  // A/B switch for the node format
-            if (std::atoi(w) == 2) sc.bvh_width = 2;
+        sc.nodes8 = pt->bvh.nodes8;
+        sc.root_link8 = pt->bvh.root_link8;
+        sc.bvh_width = pt->bvh_width;
     }
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pt->device);
     sc.num_cus = (uint32_t)std::max(1, cus);
     sc.trace_refill = 24;  // persistent BVH4 kernels; 0 selects the one-ray-per-lane kernels (A/B)
     if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
-    if (pt->two_level && sc.trace_refill == 0) sc.trace_refill = 24;  // two-level: persistent BVH4 kernels only
+    if ((pt->two_level || sc.bvh_width == 8) && sc.trace_refill == 0) sc.trace_refill = 24;  // persistent kernels only
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
@@ -599,9 +604,11 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
     pt->totals.bvh_nodes = pt->two_level ? two_level_nodes(pt->tl)
-                           : (pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes);
+                           : (pt->sc.bvh_width == 8 ? pt->bvh.num_nodes8
+                                                    : (pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes));
     pt->totals.two_level = pt->two_level ? 1u : 0u;
-    pt->totals.bvh_depth = pt->two_level ? pt->tl.tlas_depth + pt->tl.blas_depth : pt->bvh.depth4;
+    pt->totals.bvh_depth = pt->two_level ? pt->tl.tlas_depth + pt->tl.blas_depth
+                                         : (pt->sc.bvh_width == 8 ? pt->bvh.depth8 : pt->bvh.depth4);
     pt->totals.bvh_prims = pt->num_prims;
     pt->totals.build_ms = pt->build_ms;
     *out = pt;
@@ -644,7 +651,8 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
         return PUPIL_OK;
     }
     BvhBuildInput bin{pt->num_prims, pt->d_prim_inst, pt->d_insts, pt->d_mats};
-    // refit in place (PUPIL_FLAT_UPDATE=rebuild, or the BVH2 A/B node format: full rebuild)
+    bin.wide8 = pt->sc.bvh_width == 8 ? 1u : 0u;
+    // refit in place (PUPIL_FLAT_UPDATE=rebuild, or the BVH2 / BVH8 node formats: full rebuild)
     const char *fu = std::getenv("PUPIL_FLAT_UPDATE");
     if (pt->sc.bvh_width == 4 && !(fu && std::strcmp(fu, "rebuild") == 0)) {
         double rms = 0.0;
@@ -669,8 +677,10 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     pt->sc.root_link = nb.root_link;
     pt->sc.nodes4 = nb.nodes4;
     pt->sc.root_link4 = nb.root_link4;
-    pt->totals.bvh_nodes = pt->sc.bvh_width == 4 ? nb.num_nodes4 : nb.num_nodes;
-    pt->totals.bvh_depth = nb.depth4;
+    pt->sc.nodes8 = nb.nodes8;
+    pt->sc.root_link8 = nb.root_link8;
+    pt->totals.bvh_nodes = pt->sc.bvh_width == 8 ? nb.num_nodes8 : (pt->sc.bvh_width == 4 ? nb.num_nodes4 : nb.num_nodes);
+    pt->totals.bvh_depth = pt->sc.bvh_width == 8 ? nb.depth8 : nb.depth4;
     pt->totals.build_ms = ms;
     return PUPIL_OK;
 }
@@ -809,7 +819,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
             // (grouping the next list by direction octant measured slower: 21.2 vs 20.8 ms extend)
             launch_partition(pt->ps.sflags, np, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
                              q.counts + kStartNext, nullptr, b < 128 ? pt->ray_log + 2 * b : nullptr, s);
-            if (pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill) {
+            if (pt->mixed_trace && pt->sc.bvh_width >= 4 && pt->sc.trace_refill) {
                 ev0(1);
                 tail_slot();
                 launch_trace_mixed(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);

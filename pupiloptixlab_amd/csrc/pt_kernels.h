@@ -12,6 +12,7 @@ namespace pupil {
 
 constexpr int kTraceBlock = 128;
 constexpr int kTraceWavesPerSimd = 7;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8: 2 % slower)
+constexpr int kTraceWavesPerSimd8 = 5;  // BVH8 kernels (<= 96 VGPRs; 6 waves spill 17 registers: 24.2 vs 23.7 ms)
 constexpr int kTraceWavesPerSimdTL = 5;  // two-level variant (<= 96 VGPRs; A/B r02 on config 5: 4 waves 688, 5: 743, 6: 716 Mrays/s)
 constexpr int kStackLds = 32;   // per-thread LDS stack entries
 constexpr int kStackOvf = 160;  // per-thread global overflow entries
@@ -21,6 +22,10 @@ constexpr int kRing = 16;       // persistent BVH4 kernels: per-lane LDS ring en
 // (or rebuilt with the depth-bounded Karras LBVH) at create time, so no kernel ever
 // overwrites a live entry.
 constexpr int kTraceStackEntries = kRing + kStackOvf < kStackLds + kStackOvf ? kRing + kStackOvf : kStackLds + kStackOvf;
+// BVH8 kernels: stack entries are (base, bits) pairs: kRing8 in the LDS ring, the
+// overflow column's kStackOvf ints hold kStackOvf / 2 more
+constexpr int kRing8 = 8;
+constexpr int kTrace8StackEntries = kRing8 + kStackOvf / 2;
 constexpr int kShadeBlock = 256;
 constexpr uint32_t kMaxDepth = 128;  // PTPass inspector range (pt_pass.cpp:225-237)
 constexpr uint32_t kNumQueues = 9;  // 0 = miss, 1..7 = EMatType, 8 = unknown material
@@ -143,10 +148,12 @@ struct BvhBuildInput {
     const DevInstance *instances;   // device
     const DevMaterial *materials;   // device
     uint32_t object_space;          // 1: BLAS build (vertices untransformed, shading records in primitive order)
+    uint32_t wide8 = 0;             // 1: collapse to the 8-wide Bvh8Node tree instead of the BVH4 (flat scenes)
 };
 struct BvhBuildOutput {
     BvhNode *nodes;     // device, max(1, n-1)
-    Bvh4Node *nodes4;   // device, collapsed 4-wide quantized tree
+    Bvh4Node *nodes4;   // device, collapsed 4-wide quantized tree (null for wide8 builds)
+    Bvh8Node *nodes8;   // device, wide8 builds: 8-wide tree; records at kLeafSlots * node + slot
     float4 *prims;      // device, 3 * n
     float4 *attrs;      // device, kAttrStride * n shading records (same order)
     uint32_t root_link;
@@ -154,6 +161,10 @@ struct BvhBuildOutput {
     uint32_t num_nodes;
     uint32_t num_nodes4;
     uint32_t depth4;    // levels of the BVH4 (1 = root only); 0 = not measured (A/B collapse)
+    uint32_t num_nodes8 = 0;
+    uint32_t depth8 = 0;      // levels of the BVH8
+    uint32_t root_link8 = 0;
+    uint32_t num_records = 0; // primitive records (wide8: kLeafSlots per node, with holes)
     // first node of each BVH4 level (breadth-first collapse order) and the end; empty when
     // not measured.  Children always lie on a later level (bottom-up refits walk it backwards).
     std::vector<uint32_t> level_start;

@@ -110,6 +110,24 @@ struct alignas(64) Bvh4Node {
     uint32_t qhi_x, qhi_y, qhi_z;
     uint32_t pad[2];
 };
+// 8-wide node (PUPIL_BVH_WIDTH=8, flattened BVH): one 128-B line, 80 B read.
+// Child slot k: box quantized like Bvh4Node (planes in byte k % 4 of word k / 4);
+// internal children (imask bit k) are nodes child_base + (internal slots below k),
+// so a stack entry is a whole node group (child_base, slot hit bits, imask); a leaf
+// child in slot k holds up to 2 primitives, records kLeafSlots * node + 2k + {0, 1}
+// (pvalid bit 2k + j: record present).  Slots are assigned by the child's centroid
+// offset octant (Ylitie et al. 2017), so slot k ^ octant(ray) orders a node's
+// children roughly front to back.
+struct alignas(128) Bvh8Node {
+    float ox, oy, oz;
+    uint32_t exps;        // e_x | e_y << 8 | e_z << 16 | imask << 24
+    uint32_t child_base;  // first internal child node
+    uint32_t pvalid;      // bits 0..15: record slots holding a primitive
+    uint32_t pad0[2];
+    uint32_t qlo_x[2], qhi_x[2], qlo_y[2], qhi_y[2], qlo_z[2], qhi_z[2];
+    uint32_t pad1[12];
+};
+constexpr uint32_t kLeafSlots = 16;  // primitive record slots per Bvh8Node
 constexpr int kEmptyLink = 0x7FFFFFFF;
 // Traversal terminator (stack bottom); also the root link of an empty scene.
 // Inner-node links are < kTraverseDone, leaf links are negative.
@@ -136,12 +154,14 @@ struct Camera {
 struct DeviceScene {
     const BvhNode *nodes;
     const Bvh4Node *nodes4;
+    const Bvh8Node *nodes8;  // bvh_width 8: records at kLeafSlots * node + slot
     const float4 *prims;  // 3 float4 per primitive, Morton order
     const float4 *attrs;  // kAttrStride float4 per primitive, same order (hit reconstruction)
     uint32_t num_prims;
     uint32_t root_link;   // link of the root (internal 0 or a leaf), BVH2
     uint32_t root_link4;  // same for the BVH4
-    uint32_t bvh_width;   // 2 or 4: which node array the traversal kernels use
+    uint32_t root_link8;  // BVH8: 0 = node 0, a leaf link = records [0, n), kTraverseDone = empty
+    uint32_t bvh_width;   // 2, 4 or 8: which node array the traversal kernels use
     uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
     uint32_t num_cus;       // compute units of the device (persistent grid size)
     uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node

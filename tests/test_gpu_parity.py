@@ -77,7 +77,7 @@ def _cornell(res, depth=4):
     return World().load_scene(scenes.cornell_xml(os.path.join(TMP, f"cb{res}.xml"), res, res, depth))
 
 
-@pytest.mark.parametrize("width", ["2", "4"])
+@pytest.mark.parametrize("width", ["2", "4", "8"])
 def test_primary_hits_match_oracle(width, monkeypatch):
     monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
     w = _cornell(96)
@@ -149,10 +149,13 @@ def test_config1_cornellbox_named_size():
     assert rs["shadow_rays"] <= rs["shadow_rays_reference"] <= rs["primary_rays"] * (d.max_depth - 1)
 
 
-@pytest.mark.parametrize("accel", ["flat", "two_level"])
+@pytest.mark.parametrize("accel", ["flat", "flat8", "two_level"])
 def test_materials_parity_config2(accel, monkeypatch):
     """Config 2 (all seven BSDFs, spheres + boxes) at 192^2, 8 spp, depth 6; one flattened
-    BVH, or a TLAS over the mesh and sphere instances."""
+    BVH (BVH4 or BVH8 nodes), or a TLAS over the mesh and sphere instances."""
+    if accel == "flat8":
+        monkeypatch.setenv("PUPIL_BVH_WIDTH", "8")
+        accel = "flat"
     monkeypatch.setenv("PUPIL_ACCEL", accel)
     p = scenes.cornell_materials_xml(os.path.join(TMP, "cbmat.xml"), 192, 192, 6)
     desc = World().load_scene(p).desc()
@@ -162,7 +165,7 @@ def test_materials_parity_config2(accel, monkeypatch):
     assert compare(gpu, ref, f"materials192x8-{accel}") == 192 * 192
 
 
-@pytest.mark.parametrize("width", ["2", "4"])
+@pytest.mark.parametrize("width", ["2", "4", "8"])
 def test_sphere_field_parity(width, monkeypatch):
     monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
     w = scenes.sphere_field(27, 240, 136, 4, seed=3)
@@ -198,7 +201,7 @@ def test_deep_paths_parity():
 
 
 # (PUPIL_BVH_WIDTH, PUPIL_REFILL): BVH2, BVH4 one-ray-per-lane, BVH4 persistent with several refill thresholds
-TRAVERSALS = [("2", "16"), ("4", "0"), ("4", "1"), ("4", "16"), ("4", "64")]
+TRAVERSALS = [("2", "16"), ("4", "0"), ("4", "1"), ("4", "16"), ("4", "64"), ("8", "1"), ("8", "24"), ("8", "64")]
 
 
 def _trace(desc, rays, any_hit=0, tmin=0.001, tmax=1e16):
