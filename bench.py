@@ -438,10 +438,10 @@ def native_oracle():
 
 
 def cpu_baseline(desc, args, pt):
-    """The CPU oracle (scalar C++ restatement of the same integrator, its own
-    binned-SAH BVH2) on a bounded sample of the same frame: every k-th pixel, all
-    spp, on every usable host CPU, timed with steady_clock.  The sampled pixels
-    are also compared with the GPU frame just rendered (bit-exact expected)."""
+    """The CPU oracle (scalar C++ restatement of the same integrator, traversing the
+    engine's own BVH4 arrays) on a bounded sample of the same frame: every k-th
+    pixel, all spp, on every usable host CPU, timed with steady_clock.  The sampled
+    pixels are also compared with the GPU frame just rendered (bit-exact expected)."""
     native = native_oracle()
     if native:
         os.environ["PUPIL_ORACLE_LIB"] = native
@@ -453,6 +453,9 @@ def cpu_baseline(desc, args, pt):
 
     threads = args.cpu_threads or usable_cpus()
     osc = oracle.OracleScene(desc)
+    exported = pt.export_bvh4()  # the CPU traverses the GPU's own BVH arrays
+    if exported is not None:
+        osc.use_bvh4(*exported)
     npix = args.width * args.height
     pixels = np.arange(0, npix, args.cpu_sample_stride, dtype=np.uint32)
     r = osc.render(spp=args.spp, max_depth=args.max_depth, pixels=pixels, threads=threads)
@@ -476,7 +479,9 @@ def cpu_baseline(desc, args, pt):
                       f"{rays} rays in {s['seconds']:.2f}s",
             "cpu": cpu_model, "host_cpus": os.cpu_count(), "usable_cpus": usable_cpus(),
             "build": "g++ -O3 -march=native (built on this host)" if native else "prebuilt -march=x86-64-v2",
-            "bvh": "the oracle's own binned-SAH BVH2 (not the engine's BVH4; hits are BVH-independent)",
+            "bvh": ("the engine's own BVH4 arrays (pupil_pt_export_bvh4: the same nodes and records the GPU "
+                    "traverses, near-to-far order, the GPU's conservative quantized box test)") if exported is not None
+            else "the oracle's own binned-SAH BVH2 (two-level scene: no flattened BVH4 to export)",
             "gpu_pixels_bit_exact": f"{exact}/{len(pixels)}"}
 
 

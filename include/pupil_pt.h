@@ -270,6 +270,12 @@ void pupil_pt_destroy(pupil_pt *pt);
  * (ox, oy, oz, dx, dy, dz, tmin, tmax); out (host) = (t, b1, b2, prim id bits)
  * per ray, prim id = 0xFFFFFFFF and t = -1 on a miss (any hit: t = 1 if occluded). */
 int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out, int any_hit);
+/* copies the flattened BVH4 the traversal kernels read (64-B quantized nodes, 12-float
+ * world-space primitive records, root link) to host memory, for the CPU baseline that
+ * traverses the same arrays.  Call with nodes = records = NULL for the
+ * counts.  PUPIL_ERR_UNSUPPORTED for the two-level structure and the BVH2 / BVH8 formats. */
+int pupil_pt_export_bvh4(pupil_pt *pt, uint32_t *num_nodes, void *nodes, uint32_t *num_records, float *records,
+                         int32_t *root_link);
 /* evaluates the device's sin, cos, acos, atan2(x, y2), sqrt, 1/x on n inputs:
  * out[6*i + k] for k in that order (bit-exactness probe for the CPU oracle) */
 int pupil_debug_math(int device, uint32_t n, const float *x, const float *y2, float *out);

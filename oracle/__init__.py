@@ -55,6 +55,8 @@ def lib():
         L.oracle_math.argtypes = [C.c_uint32, f32p, f32p, f32p]
         L.oracle_num_prims.restype = C.c_uint32
         L.oracle_num_prims.argtypes = [vp]
+        L.oracle_set_bvh4.restype = C.c_int
+        L.oracle_set_bvh4.argtypes = [vp, C.c_uint32, vp, C.c_uint32, f32p, C.c_int32]
         _LIB = L
     return _LIB
 
@@ -104,6 +106,16 @@ class OracleScene:
         out = np.zeros(6, np.float32)
         lib().oracle_camera_ray(self._h, pixel, seed, _fp(out))
         return out
+
+    def use_bvh4(self, nodes, records, root_link):
+        """Traverse the engine's own BVH4 arrays (uint8 (n, 64) nodes, float32 (m, 12)
+        world records, root link; pupil_pt_export_bvh4) instead of the oracle's BVH."""
+        nodes = np.ascontiguousarray(nodes, np.uint8).reshape(-1, 64)
+        records = np.ascontiguousarray(records, np.float32).reshape(-1, 12)
+        rc = lib().oracle_set_bvh4(self._h, len(nodes), nodes.ctypes.data_as(C.c_void_p), len(records),
+                                   _fp(records), int(root_link))
+        if rc != 0:
+            raise ValueError("engine BVH4 arrays do not match this scene")
 
     def closest(self, rays, brute_force=False):
         rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)

@@ -1143,8 +1143,26 @@ struct Node {
     unsigned int first = 0, count = 0;
 };
 
+// The engine's quantized BVH4 node (pupiloptixlab_amd/csrc/pt_scene.h Bvh4Node,
+// 64 B), for CPU traversal of the GPU's own arrays (oracle_set_bvh4): child k's
+// plane on an axis is o + q_k * 2^(e-127); link >= 0 inner node, < 0 leaf with
+// ~link = first_record << 3 | (count - 1), kQEmpty unused.
+struct QNode {
+    float ox, oy, oz;
+    uint32_t exps;
+    int32_t child[4];
+    uint32_t qlo[3], qhi[3];
+    uint32_t pad[2];
+};
+static_assert(sizeof(QNode) == 64, "Bvh4Node layout");
+constexpr int32_t kQEmpty = 0x7FFFFFFF, kQDone = 0x76543210;
+
 struct Scene {
     unsigned int width = 0, height = 0, max_depth = 1;
+    // engine BVH4 arrays (oracle_set_bvh4); empty = this file's own SAH BVH
+    std::vector<QNode> q4;
+    std::vector<uint32_t> q4_rec_prim;  // record -> primitive id (the record's a.w)
+    int32_t q4_root = kQDone;
     mat4x4 sample_to_camera{}, camera_to_world{};
     std::vector<Material> materials;
     std::vector<Instance> instances;
@@ -1242,9 +1260,85 @@ struct Scene {
         return tn <= tf * 1.0000004f;  // conservative (Ize 2013)
     }
 
+    // Child entry distances of an engine BVH4 node: the GPU's conservative
+    // quantized slab test restated (pt_kernels.hip visit4 / axis_terms): per axis
+    // t = fma(q, s * idir, (o_node - o_ray) * idir -/+ E),
+    // E = fma(512, s, |o_node - o_ray| + |o_node|) * (|idir| * 2^-21).
+    static void QVisit(const QNode &n, const Ray &r, float tmin, float tmax, float t[4]) {
+        const float o[3] = {n.ox, n.oy, n.oz}, ro[3] = {r.o.x, r.o.y, r.o.z}, id[3] = {r.idir.x, r.idir.y, r.idir.z};
+        float bn[3], an[3], af[3];
+        uint32_t qn[3], qf[3];
+        for (int a = 0; a < 3; a++) {
+            uint32_t sb = ((n.exps >> (8 * a)) & 0xFFu) << 23;
+            float sc;
+            std::memcpy(&sc, &sb, 4);
+            const float A = o[a] - ro[a];
+            const float av = A * id[a];
+            const float e = std::fma(512.f, sc, std::fabs(A) + std::fabs(o[a])) * (std::fabs(id[a]) * 0x1p-21f);
+            bn[a] = sc * id[a];
+            an[a] = av - e;
+            af[a] = av + e;
+            const bool pos = id[a] >= 0.f;
+            qn[a] = pos ? n.qlo[a] : n.qhi[a];
+            qf[a] = pos ? n.qhi[a] : n.qlo[a];
+        }
+        for (int k = 0; k < 4; k++) {
+            float tn = tmin, tf = tmax;
+            for (int a = 0; a < 3; a++) {
+                tn = std::fmax(std::fma((float)((qn[a] >> (8 * k)) & 0xFFu), bn[a], an[a]), tn);
+                tf = std::fmin(std::fma((float)((qf[a] >> (8 * k)) & 0xFFu), bn[a], af[a]), tf);
+            }
+            t[k] = (tn <= tf && n.child[k] != kQEmpty) ? tn : INFINITY;
+        }
+    }
+    // closest hit / any hit over the engine's BVH4: children visited near to far
+    bool QTrace(const Ray &r, float tmin, float tmax, bool any, unsigned int &prim, float &t, float &b1, float &b2,
+                uint64_t *nodes_visited) const {
+        if (q4_root == kQDone) return false;
+        bool found = false;
+        unsigned int best = 0xFFFFFFFFu;
+        int32_t stack[512];
+        int sp = 0;
+        stack[sp++] = q4_root;
+        while (sp) {
+            const int32_t link = stack[--sp];
+            if (link < 0) {
+                const uint32_t first = ((uint32_t)~link) >> 3, count = (((uint32_t)~link) & 7u) + 1u;
+                for (uint32_t i = first; i < first + count; i++) {
+                    const Prim &p = prims[q4_rec_prim[i]];
+                    float tt, u = 0.f, v = 0.f;
+                    const bool hit = p.sphere ? HitSphere(instances[p.inst], r, tmin, tmax, tt)
+                                              : HitTriangle(r, p, tmin, tmax, tt, u, v);
+                    if (hit && any) return true;
+                    if (hit && (tt < tmax || p.id < best)) {
+                        tmax = tt;
+                        best = p.id;
+                        t = tt;
+                        b1 = u;
+                        b2 = v;
+                        found = true;
+                    }
+                }
+                continue;
+            }
+            if (nodes_visited) (*nodes_visited)++;
+            const QNode &n = q4[(size_t)link];
+            float tk[4];
+            QVisit(n, r, tmin, tmax, tk);
+            int order[4] = {0, 1, 2, 3};  // insertion sort, far to near
+            for (int a = 1; a < 4; a++)
+                for (int b = a; b > 0 && tk[order[b]] > tk[order[b - 1]]; b--) std::swap(order[b], order[b - 1]);
+            for (int j = 0; j < 4; j++)  // farthest first, the nearest ends on top
+                if (tk[order[j]] != INFINITY && sp < 512) stack[sp++] = n.child[order[j]];
+        }
+        prim = best;
+        return found;
+    }
+
     // optixTrace closest hit; ties broken by the smaller primitive id
     bool Closest(const Ray &r, float tmin, float tmax, unsigned int &prim, float &t, float &b1, float &b2,
                  uint64_t *nodes_visited = nullptr) const {
+        if (!q4_rec_prim.empty()) return QTrace(r, tmin, tmax, false, prim, t, b1, b2, nodes_visited);
         bool found = false;
         unsigned int best = 0xFFFFFFFFu;
         int stack[128];
@@ -1279,6 +1373,11 @@ struct Scene {
     }
     // shadow rays: TERMINATE_ON_FIRST_HIT
     bool Occluded(const Ray &r, float tmin, float tmax) const {
+        if (!q4_rec_prim.empty()) {
+            unsigned int prim;
+            float t, b1, b2;
+            return QTrace(r, tmin, tmax, true, prim, t, b1, b2, nullptr);
+        }
         int stack[128];
         int sp = 0;
         stack[sp++] = 0;
@@ -1592,6 +1691,28 @@ oracle_scene *oracle_scene_create(const pupil_scene_desc *d) {
 }
 
 void oracle_scene_destroy(oracle_scene *s) { delete reinterpret_cast<oracle::Scene *>(s); }
+
+// Traverse the engine's own BVH4 (pupil_pt_export_bvh4: 64-B nodes, 12-float world
+// records whose a.w holds the primitive id | sphere bit) instead of this file's BVH;
+// the primitives are still tested on this file's data.  num_records = 0 restores it.
+int oracle_set_bvh4(oracle_scene *s, uint32_t num_nodes, const void *nodes, uint32_t num_records,
+                    const float *records, int32_t root_link) {
+    auto &sc = *reinterpret_cast<oracle::Scene *>(s);
+    sc.q4.assign(reinterpret_cast<const oracle::QNode *>(nodes), reinterpret_cast<const oracle::QNode *>(nodes) + num_nodes);
+    sc.q4_rec_prim.resize(num_records);
+    for (uint32_t i = 0; i < num_records; i++) {
+        uint32_t bits;
+        std::memcpy(&bits, &records[12 * i + 3], 4);
+        bits &= 0x7FFFFFFFu;  // sphere bit
+        if (bits >= sc.prims.size()) return -1;
+        sc.q4_rec_prim[i] = bits;
+    }
+    sc.q4_root = root_link;
+    for (const auto &n : sc.q4)
+        for (int k = 0; k < 4; k++)
+            if (n.child[k] >= 0 && n.child[k] != oracle::kQEmpty && (uint32_t)n.child[k] >= num_nodes) return -1;
+    return 0;
+}
 
 // spp consecutive OnRun frames (pt_pass.cpp:51-56) over the given pixels.
 // pixels == NULL renders the whole image (out index = pixel index).

@@ -116,6 +116,7 @@ SIGNATURES = {
                                          u32p, u32p]),
     "pupil_pt_destroy": (None, [C.c_void_p]),
     "pupil_pt_trace_rays": (C.c_int, [C.c_void_p, C.c_uint32, f32p, f32p, C.c_int]),
+    "pupil_pt_export_bvh4": (C.c_int, [C.c_void_p, u32p, C.c_void_p, u32p, f32p, C.POINTER(C.c_int32)]),
     "pupil_debug_math": (C.c_int, [C.c_int, C.c_uint32, f32p, f32p, f32p]),
     "pupil_image_save": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, f32p, C.c_uint32]),
     "pupil_debug_select_emitter": (C.c_int, [C.c_void_p, C.c_uint32, f32p, C.POINTER(C.c_int32)]),

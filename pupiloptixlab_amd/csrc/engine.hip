@@ -937,6 +937,24 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
 
 void pupil_pt_destroy(pupil_pt *pt) { delete pt; }
 
+int pupil_pt_export_bvh4(pupil_pt *pt, uint32_t *num_nodes, void *nodes, uint32_t *num_records, float *records,
+                         int32_t *root_link) {
+    if (!pt || !num_nodes || !num_records || !root_link) return fail(PUPIL_ERR_INVALID, "null argument");
+    if (pt->two_level || pt->sc.bvh_width != 4) return fail(PUPIL_ERR_UNSUPPORTED, "only the flattened BVH4 is exported");
+    HIP_TRY(hipSetDevice(pt->device));
+    const uint32_t nn = pt->bvh.num_nodes4, nr = pt->bvh.num_records;
+    if (nodes || records) {
+        if (*num_nodes < nn || *num_records < nr) return fail(PUPIL_ERR_INVALID, "output too small");
+        HIP_TRY(hipDeviceSynchronize());
+        if (nodes && nn) HIP_TRY(hipMemcpy(nodes, pt->bvh.nodes4, sizeof(Bvh4Node) * nn, hipMemcpyDeviceToHost));
+        if (records && nr) HIP_TRY(hipMemcpy(records, pt->bvh.prims, sizeof(float4) * 3 * (size_t)nr, hipMemcpyDeviceToHost));
+    }
+    *num_nodes = nn;
+    *num_records = nr;
+    *root_link = (int32_t)pt->bvh.root_link4;
+    return PUPIL_OK;
+}
+
 int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out, int any_hit) {
     if (!pt || !rays || !out) return fail(PUPIL_ERR_INVALID, "null argument");
     if (n == 0) return PUPIL_OK;

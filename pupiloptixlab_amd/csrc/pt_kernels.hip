@@ -626,7 +626,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     if (STATS && stats.wave_times) t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t p = 0, best_key = 0, best_idx = kMissIndex;
     RayPre r{};
-    float tmin = 0.f, tmax = 0.f, b1 = 0.f, b2 = 0.f;
+    float tmin = MODE == kModeRays ? 0.f : 0.001f, tmax = 0.f, b1 = 0.f, b2 = 0.f;  // tmin: a constant outside kModeRays
     int node = kSentinel, leaf = 0;
     bool found = false;
     bool any = ANY;  // this lane's ray terminates on its first hit
@@ -1045,7 +1045,7 @@ __device__ __forceinline__ void trace8_body(const DeviceScene &sc, const PathSta
     if (STATS && stats.wave_times) t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t p = 0, best_key = 0, best_idx = kMissIndex;
     RayPre r{};
-    float tmin = 0.f, tmax = 0.f, b1 = 0.f, b2 = 0.f;
+    float tmin = MODE == kModeRays ? 0.f : 0.001f, tmax = 0.f, b1 = 0.f, b2 = 0.f;  // tmin: a constant outside kModeRays
     uint32_t gbase = 0, gbits = 0, tbase = 0, tbits = 0, oct = 0;
     bool found = false;
     bool any = ANY;

@@ -240,6 +240,20 @@ class PTPass(Pass):
         check(self._lib.pupil_pt_stats(self._pt, C.byref(c)))
         return c.as_dict()
 
+    def export_bvh4(self):
+        """The flattened BVH4 the traversal kernels read: (uint8 (n, 64) nodes, float32 (m, 12)
+        world records, root link), or None for the two-level structure / other node formats."""
+        import numpy as np
+
+        nn, nr, root = C.c_uint32(0), C.c_uint32(0), C.c_int32(0)
+        if self._lib.pupil_pt_export_bvh4(self._pt, C.byref(nn), None, C.byref(nr), None, C.byref(root)) != 0:
+            return None
+        nodes = np.zeros((max(1, nn.value), 64), np.uint8)
+        recs = np.zeros((max(1, nr.value), 12), np.float32)
+        check(self._lib.pupil_pt_export_bvh4(self._pt, C.byref(nn), nodes.ctypes.data_as(C.c_void_p), C.byref(nr),
+                                             recs.ctypes.data_as(C.POINTER(C.c_float)), C.byref(root)))
+        return nodes[: nn.value], recs[: nr.value], root.value
+
     def image(self, name: str = FINAL_RESULT):
         """Full-frame (h, w, c) numpy image, row 0 = bottom (reference pixel order)."""
         t = self.buffers.get(name).cpu().numpy()

@@ -646,3 +646,33 @@ def test_builtin_sphere_update_refit_equals_fresh_engine(accel, update, monkeypa
     pt.close_engine()
     fresh = render_gpu(w.desc(), 2)["pt accum buffer"]
     assert np.array_equal(moved.view(np.uint32), fresh.view(np.uint32))
+
+
+def test_cpu_oracle_on_the_engine_bvh4_arrays():
+    """SURVEY §8(d) CPU baseline: the oracle traverses the GPU's own BVH4 arrays
+    (pupil_pt_export_bvh4) and renders the same frame bit for bit; closest hits of
+    random rays agree with the oracle's own BVH."""
+    import torch
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    desc = scenes.sphere_field(27, 160, 90, 4, seed=4).desc()
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    pt.dirty = False
+    pt.render(2)
+    torch.cuda.synchronize()
+    gpu = pt.buffers.get("pt accum buffer").cpu().numpy()
+    nodes, recs, root = pt.export_bvh4()
+    pt.close_engine()
+    assert len(nodes) > 1 and len(recs) == oracle.OracleScene(desc).num_prims and root == 0
+    own = oracle.OracleScene(desc)
+    q4 = oracle.OracleScene(desc)
+    q4.use_bvh4(nodes, recs, root)
+    ref = q4.render(spp=2)
+    assert np.array_equal(gpu.view(np.uint32), ref["accum"].view(np.uint32))
+    rng = np.random.default_rng(5)
+    org = rng.uniform([-7.5, 0.1, -9.5], [7.5, 13.9, 13.5], (20000, 3))
+    d = rng.normal(size=(20000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([org, d], 1).astype(np.float32)
+    assert np.array_equal(q4.closest(rays).view(np.uint32), own.closest(rays).view(np.uint32))
