@@ -1,9 +1,10 @@
 #!/bin/bash
-# Bench sweep over traversal knobs: SWEEP="refill:node_min ..." (PUPIL_REFILL / PUPIL_NODE_MIN)
+# Env-knob sweep on the default config-4 bench (VARS: ';'-separated env settings).
 set -u
-mkdir -p gpurun_out
-for c in ${SWEEP:-32:1}; do
-  r=${c%%:*}; nm=${c##*:}
-  PUPIL_REFILL=$r PUPIL_NODE_MIN=$nm timeout -k 10 300 python bench.py --steps 3 --warmup 1 --cpu-baseline 0 > gpurun_out/sw_${r}_${nm}.log 2>&1 || exit 1
-  python3 -c "import json; d=json.loads(open('gpurun_out/sw_${r}_${nm}.log').read().strip().splitlines()[-1]); print('refill $r node_min $nm', d['value'], d['ms_per_step'], d['config']['stage_ms_per_frame'])"
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/sweep
+IFS=';' read -r -a V <<< "${VARS:?}"
+for v in "${V[@]}"; do
+  env $v timeout -k 10 300 python bench.py --steps ${STEPS:-5} --warmup 2 --cpu-baseline 0 --dropin 0 ${BENCH_ARGS:-} > gpurun_out/sweep/b.log 2>&1 || { echo "$v failed"; tail -n 5 gpurun_out/sweep/b.log; exit 1; }
+  echo "$v $(tail -n1 gpurun_out/sweep/b.log | grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"stage_ms_per_frame": {[^}]*}' | tr '\n' ' ')"
 done
