@@ -38,6 +38,17 @@
 #include <vector>
 
 #include "../include/pupil_detmath.h"
+#ifdef ORACLE_SYSTEM_LIBM
+// Test build only (tests/test_detmath.py): the host's libm instead of the shared
+// deterministic one, to show the choice of libm does not bias the image.
+namespace oracle_syslibm {
+inline float dm_sin(float x) { return std::sin(x); }
+inline float dm_cos(float x) { return std::cos(x); }
+inline float dm_acos(float x) { return std::acos(x); }
+inline float dm_atan2(float y, float x) { return std::atan2(y, x); }
+}  // namespace oracle_syslibm
+#define pupil_dm oracle_syslibm
+#endif
 #include "../include/pupil_pt.h"
 
 namespace oracle {
