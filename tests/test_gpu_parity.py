@@ -676,3 +676,45 @@ def test_cpu_oracle_on_the_engine_bvh4_arrays():
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.concatenate([org, d], 1).astype(np.float32)
     assert np.array_equal(q4.closest(rays).view(np.uint32), own.closest(rays).view(np.uint32))
+
+
+def test_consecutive_launches_on_one_engine():
+    """The persistent kernels reset their own dequeue heads and exit counters (the
+    last wave out, pt_kernels.hip trace4_body): eight renders on ONE engine with
+    changing seeds, depths and tilings, then ray queries of awkward sizes, each equal
+    to the oracle -- a dropped or repeated work item would change a pixel or a count."""
+    import torch
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    desc = scenes.sphere_field(27, 96, 64, 4, seed=6).desc()
+    o = oracle.OracleScene(desc)
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    n = 96 * 64
+    for k, (depth, spp, tile) in enumerate([(4, 2, None), (1, 1, None), (2, 3, (16, 1, 3)), (6, 1, None),
+                                            (3, 2, (8, 0, 2)), (4, 1, (8, 1, 2)), (5, 2, None), (4, 1, None)]):
+        pt.set_tiling(*(tile or (32, 0, 1)))
+        pt.max_depth = depth
+        pt.dirty = False
+        pt.random_seed, pt.sample_cnt = 10 + k, 0
+        pt.render(spp, collect_stats=True)
+        torch.cuda.synchronize()
+        got = pt.buffers.get("pt accum buffer").cpu().numpy()
+        pix = pt.local_pixels() if tile else np.arange(n, dtype=np.uint32)
+        ref = o.render(spp=spp, random_seed=10 + k, max_depth=depth, pixels=pix)
+        assert np.array_equal(got.view(np.uint32), ref["accum"].view(np.uint32)), f"render {k}"
+        s, rs = pt.stats(), ref["stats"]
+        assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
+            (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"]), f"render {k}"
+    rng = np.random.default_rng(3)
+    for m in (1, 63, 64, 65, 4097, 300001):
+        org = rng.uniform([-7.5, 0.1, -9.5], [7.5, 13.9, 13.5], (m, 3))
+        d = rng.normal(size=(m, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        rays = np.concatenate([org, d], 1).astype(np.float32)
+        r8 = np.ascontiguousarray(np.concatenate([rays, np.full((m, 1), 0.001, np.float32),
+                                                  np.full((m, 1), 1e16, np.float32)], 1), np.float32)
+        out = np.zeros((m, 4), np.float32)
+        abi.check(pt._lib.pupil_pt_trace_rays(pt._pt, m, r8.ctypes.data_as(abi.f32p), out.ctypes.data_as(abi.f32p), 0))
+        assert np.array_equal(out.view(np.uint32), o.closest(rays).view(np.uint32)), f"{m} rays"
+    pt.close_engine()
