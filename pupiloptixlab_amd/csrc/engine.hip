@@ -90,6 +90,7 @@ struct pupil_pt {
     BvhBuildOutput bvh{};
     bool two_level = false;  // TLAS + per-shape BLAS (accel_two_level.hip) instead of one flattened BVH
     uint32_t bvh_width = 4;  // flattened BVH node format (PUPIL_BVH_WIDTH)
+    bool primary_interleave = true;  // primary extend dequeues pixel-major (PUPIL_PRIMARY_ORDER)
     TwoLevelAccel tl{};
     uint32_t width = 0, height = 0, max_depth = 1;
     uint32_t num_prims = 0;
@@ -584,6 +585,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     sc.trace_refill = 24;  // persistent BVH4 kernels; 0 selects the one-ray-per-lane kernels (A/B)
     if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
     if ((pt->two_level || sc.bvh_width == 8) && sc.trace_refill == 0) sc.trace_refill = 24;  // persistent kernels only
+    if (const char *po = std::getenv("PUPIL_PRIMARY_ORDER")) pt->primary_interleave = std::strcmp(po, "path") != 0;
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
@@ -805,7 +807,9 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     launch_generate(pt->sc, fp, pt->ps, s);
     ev0(0);
     tail_slot();
-    launch_extend(pt->sc, pt->ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s);
+    // camera rays: the spp samples of a pixel on consecutive lanes (PUPIL_PRIMARY_ORDER=path: path order)
+    launch_extend(pt->sc, pt->ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s,
+                  pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u, fp.num_local);
     ev1();
     bin_paths();
     for (uint32_t b = 0; b < bounces; b++) {

@@ -117,9 +117,11 @@ struct TraceStats {
 
 // wavefront stages
 void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, hipStream_t s);
+// interleave_spp / num_local (primary extend, queue == null): dequeue the spp samples of
+// a pixel on consecutive lanes (TraceJob::spp); 0 = path order
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
                    const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
-                   const TraceStats *stats, hipStream_t s);
+                   const TraceStats *stats, hipStream_t s, uint32_t interleave_spp = 0, uint32_t num_local = 0);
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,
                   uint32_t bounce, hipStream_t s);
 void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,

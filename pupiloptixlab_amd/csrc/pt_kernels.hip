@@ -489,6 +489,11 @@ struct TraceJob {
     uint32_t node_min;          // node phase ends when fewer lanes than this still need a node (>= 1)
     const float *rays;          // kModeRays: 8 floats per ray (o, d, tmin, tmax)
     float *out;                 // kModeRays: 4 floats per ray
+    // primary extend (queue == null): list position i -> path (i % spp) * num_local + i / spp,
+    // so consecutive lanes take the spp samples of one pixel (coherent camera rays) while
+    // path ids stay sample major; spp = 0: identity
+    uint32_t spp;
+    uint32_t num_local;
 };
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
@@ -675,7 +680,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 if (k < len) {
                     float4 o, d;
                     if (MODE == kModeExtend) {
-                        p = job.queue ? job.queue[i] : i;
+                        p = job.queue ? job.queue[i] : (job.spp ? (i % job.spp) * job.num_local + i / job.spp : i);
                         o = ps.ray_o[p];
                         d = ps.ray_d[p];
                         tmin = 0.001f;
@@ -1086,7 +1091,7 @@ __device__ __forceinline__ void trace8_body(const DeviceScene &sc, const PathSta
                 if (k < len) {
                     float4 o, d;
                     if (MODE == kModeExtend) {
-                        p = job.queue ? job.queue[i] : i;
+                        p = job.queue ? job.queue[i] : (job.spp ? (i % job.spp) * job.num_local + i / job.spp : i);
                         o = ps.ray_o[p];
                         d = ps.ray_d[p];
                         tmin = 0.001f;
@@ -1764,7 +1769,7 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
                         uint32_t ovf_threads, uint32_t *work, hipStream_t s) {
     if ((sc.bvh_width == 4 || sc.bvh_width == 8) && sc.trace_refill) {  // the production kernel, fed from a ray array
-        const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, sc.trace_node_min, rays, out};
+        const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, sc.trace_node_min, rays, out, 0u, 0u};
         const uint32_t blocks = trace4_blocks(sc, ovf_threads);
         if (sc.bvh_width == 8) {
             if (any)
@@ -1818,12 +1823,13 @@ void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathSta
 
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
                    const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
-                   const TraceStats *stats, hipStream_t s) {
+                   const TraceStats *stats, hipStream_t s, uint32_t interleave_spp, uint32_t num_local) {
     const uint32_t blocks = ovf_threads / kTraceBlock;
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
     if ((w4 || sc.bvh_width == 8) && sc.trace_refill) {
-        const TraceJob job{queue, queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
+        const TraceJob job{queue,   queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min,
+                           nullptr, nullptr,     queue ? 0u : interleave_spp, num_local};
         launch_trace4<kModeExtend, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
         return;
     }
@@ -1846,7 +1852,7 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
     TraceStats st = stats ? *stats : TraceStats{nullptr};
     const bool w4 = sc.bvh_width == 4;
     if ((w4 || sc.bvh_width == 8) && sc.trace_refill) {
-        const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkShadow, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
+        const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkShadow, sc.trace_refill, sc.trace_node_min, nullptr, nullptr, 0u, 0u};
         launch_trace4<kModeShadow, true>(sc, ps, q, job, ovf, ovf_threads, stats, s);
         return;
     }
@@ -1864,7 +1870,7 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
 
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                         const TraceStats *stats, hipStream_t s) {
-    const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr};
+    const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr, 0u, 0u};
     launch_trace4<kModeMixed, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
 }
 
