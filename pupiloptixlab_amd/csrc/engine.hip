@@ -91,6 +91,7 @@ struct pupil_pt {
     bool two_level = false;  // TLAS + per-shape BLAS (accel_two_level.hip) instead of one flattened BVH
     uint32_t bvh_width = 4;  // flattened BVH node format (PUPIL_BVH_WIDTH)
     bool primary_interleave = true;  // primary extend dequeues pixel-major (PUPIL_PRIMARY_ORDER)
+    bool shade_list = false;  // shade walks the traced list instead of a material partition (PUPIL_SHADE_LIST)
     TwoLevelAccel tl{};
     uint32_t width = 0, height = 0, max_depth = 1;
     uint32_t num_prims = 0;
@@ -586,6 +587,15 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
     if ((pt->two_level || sc.bvh_width == 8) && sc.trace_refill == 0) sc.trace_refill = 24;  // persistent kernels only
     if (const char *po = std::getenv("PUPIL_PRIMARY_ORDER")) pt->primary_interleave = std::strcmp(po, "path") != 0;
+    {  // one material bin in the whole scene: the material partition orders nothing (auto; =bins / =list force)
+        uint32_t bins = 0;
+        for (const DevInstance &d : insts) bins |= 1u << d.bin;
+        pt->shade_list = (bins & (bins - 1u)) == 0u;
+        if (const char *sl = std::getenv("PUPIL_SHADE_LIST")) {
+            if (std::strcmp(sl, "bins") == 0) pt->shade_list = false;
+            if (std::strcmp(sl, "list") == 0) pt->shade_list = true;
+        }
+    }
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
@@ -811,12 +821,12 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     launch_extend(pt->sc, pt->ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s,
                   pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u, fp.num_local);
     ev1();
-    bin_paths();
+    if (!pt->shade_list) bin_paths();
     for (uint32_t b = 0; b < bounces; b++) {
         const uint32_t tag = sflag_tag(fp.max_depth, b);
         if (tag == 0) HIP_TRY(hipMemsetAsync(pt->ps.sflags, 0, np, s));
         ev0(2);
-        launch_shade(pt->sc, fp, pt->ps, q, b, s);
+        launch_shade(pt->sc, fp, pt->ps, q, b, s, !pt->shade_list ? kShadeBins : (b == 0 ? kShadeAll : kShadeNext));
         ev1();
         if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
             // next (bit 0) and shadow (bit 1) lists -> q.nxsh, each in increasing path order
@@ -836,7 +846,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
                 launch_extend(pt->sc, pt->ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, tsp, s);
                 ev1();
             }
-            bin_paths();
+            if (!pt->shade_list) bin_paths();
         }
     }
     launch_accumulate(fp, pt->ps, s);

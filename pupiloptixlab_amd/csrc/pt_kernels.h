@@ -122,8 +122,11 @@ void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathSta
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
                    const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
                    const TraceStats *stats, hipStream_t s, uint32_t interleave_spp = 0, uint32_t num_local = 0);
+// which paths a shade launch walks: the material-bin partition (q.bins), every path
+// (after the primary extend), or the previous bounce's next list (q.nxsh)
+enum ShadeList : int { kShadeBins = 0, kShadeAll = 1, kShadeNext = 2 };
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,
-                  uint32_t bounce, hipStream_t s);
+                  uint32_t bounce, hipStream_t s, ShadeList list = kShadeBins);
 void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                    const TraceStats *stats, hipStream_t s);
 // one persistent launch over the next + shadow lists of a bounce (BVH4 persistent path only)

@@ -1618,21 +1618,32 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
 // path order, so a wave sees one material except at the 8 bin boundaries; the
 // branch below is wave-uniform almost everywhere.  One launch instead of nine
 // per bounce keeps empty-bin launches off the frame (they cost ~4 us each).
+// SHADE_LIST (single-material scenes, ShadeList): no material partition; the launch
+// walks the paths the last traversal traced -- all paths after the primary extend,
+// else the previous bounce's next list, both in increasing path order -- and takes
+// each path's bin from the byte the traversal wrote.  Only the miss / hit split
+// diverges inside a wave, which costs less than the three partition launches.
+template <int LIST>
 __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
                                                            uint32_t bounce) {
-    const uint32_t count = q.counts[kScratch];  // all traced paths (total of the bin partition)
+    const uint32_t count = LIST == kShadeBins ? q.counts[kScratch]  // all traced paths (total of the bin partition)
+                                              : (LIST == kShadeAll ? fp.num_paths : q.counts[kCntNext]);
     const uint32_t tag = sflag_tag(fp.max_depth, bounce);
     uint32_t start[kPartMaxBins];
 #pragma unroll
-    for (int b = 0; b < kPartMaxBins; b++) start[b] = q.counts[kStartBins + b];
+    for (int b = 0; b < kPartMaxBins; b++) start[b] = LIST == kShadeBins ? q.counts[kStartBins + b] : 0u;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
-        const uint32_t p = q.bins[i];
+        const uint32_t p = LIST == kShadeBins ? q.bins[i] : (LIST == kShadeAll ? i : q.nxsh[i]);
         // bin of list position i: the last bin starting at or before i (an empty
         // bin starts where the next one does, so it is never the last such bin)
         uint32_t bin = 0;
+        if (LIST == kShadeBins) {
 #pragma unroll
-        for (int b = 1; b < kPartMaxBins; b++) bin = i >= start[b] ? (uint32_t)b : bin;
+            for (int b = 1; b < kPartMaxBins; b++) bin = i >= start[b] ? (uint32_t)b : bin;
+        } else {
+            bin = ps.mbin[p];
+        }
         uint32_t flags = 0;
         switch (bin) {
         case 0: shade_miss(sc, fp, ps, p, bounce); break;
@@ -1889,8 +1900,11 @@ static uint32_t shade_blocks(uint32_t num_paths) {
 }
 
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,
-                  uint32_t bounce, hipStream_t s) {
-    hipLaunchKernelGGL(k_shade_all, dim3(shade_blocks(fp.num_paths)), dim3(kShadeBlock), 0, s, sc, fp, ps, q, bounce);
+                  uint32_t bounce, hipStream_t s, ShadeList list) {
+    const dim3 g(shade_blocks(fp.num_paths)), b(kShadeBlock);
+    if (list == kShadeAll) hipLaunchKernelGGL(k_shade_all<kShadeAll>, g, b, 0, s, sc, fp, ps, q, bounce);
+    else if (list == kShadeNext) hipLaunchKernelGGL(k_shade_all<kShadeNext>, g, b, 0, s, sc, fp, ps, q, bounce);
+    else hipLaunchKernelGGL(k_shade_all<kShadeBins>, g, b, 0, s, sc, fp, ps, q, bounce);
 }
 
 void launch_accumulate(const FrameParams &fp, const PathState &ps, hipStream_t s) {

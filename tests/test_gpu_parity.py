@@ -718,3 +718,19 @@ def test_consecutive_launches_on_one_engine():
         abi.check(pt._lib.pupil_pt_trace_rays(pt._pt, m, r8.ctypes.data_as(abi.f32p), out.ctypes.data_as(abi.f32p), 0))
         assert np.array_equal(out.view(np.uint32), o.closest(rays).view(np.uint32)), f"{m} rays"
     pt.close_engine()
+
+
+@pytest.mark.parametrize("mode", ["bins", "list"])
+def test_shade_list_modes_parity(mode, monkeypatch):
+    """Shading over the material-bin partition, or over the traced list with per-path
+    bins (the default for single-material scenes), forced on a scene with all seven BSDFs."""
+    monkeypatch.setenv("PUPIL_SHADE_LIST", mode)
+    p = scenes.cornell_materials_xml(os.path.join(TMP, "cbmat96.xml"), 96, 96, 6)
+    desc = World().load_scene(p).desc()
+    gpu = render_gpu(desc, 4)
+    ref = oracle.OracleScene(desc).render(spp=4)
+    assert compare(gpu, ref, f"shade-{mode}") == 96 * 96
+    assert np.array_equal(gpu["albedo"], ref["albedo"]) and np.array_equal(gpu["normal"], ref["normal"])
+    s, rs = gpu["stats"], ref["stats"]
+    assert (s["extension_rays"], s["shadow_rays"], s["shadow_rays_reference"]) == \
+        (rs["extension_rays"], rs["shadow_rays"], rs["shadow_rays_reference"])
