@@ -97,6 +97,16 @@ struct pupil_pt {
     uint32_t num_prims = 0;
     uint32_t leaf_size = 2;  // primitives per BVH leaf (PUPIL_LEAF_SIZE)
     bool mixed_trace = true;  // one persistent launch per bounce for shadow + extension rays (PUPIL_MIXED)
+    // Render-ahead (PUPIL_AHEAD): the last mixed launch of a render also traces the
+    // camera rays of the next render (seed + spp, same camera, tiling and batch), generated
+    // into the other half of the path-state buffers, so the next render starts at its
+    // first shade and the primary extend's launch tail is gone.  1 = single-spp renders
+    // (the PTPass::OnRun cadence, pt_pass.cpp:39-57), 2 = every render, 0 = off.
+    int ahead_mode = 1;
+    bool ahead_valid = false;
+    uint32_t ahead_seed = 0, ahead_spp = 0, ahead_local = 0, ahead_half = 0;
+    uint32_t ahead_key[5] = {0, 0, 0, 0, 0};
+    hipStream_t last_stream = nullptr;
     double build_ms = 0.0;
     // path state / queues (grown on demand)
     size_t cap = 0;
@@ -159,6 +169,7 @@ struct pupil_pt {
         ps = PathState{};
         q.bins = q.nxsh = q.hist = nullptr;
         cap = 0;
+        ahead_valid = false;
     }
     ~pupil_pt() {
         (void)hipSetDevice(device);
@@ -598,6 +609,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     }
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
+    if (const char *a = std::getenv("PUPIL_AHEAD")) pt->ahead_mode = std::min(2, std::max(0, std::atoi(a)));
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     sc.prim_inst = d_prim_inst;
@@ -629,6 +641,9 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
 
 int pupil_pt_set_camera(pupil_pt *pt, const float sample_to_camera[16], const float camera_to_world[16]) {
     if (!pt || !sample_to_camera || !camera_to_world) return fail(PUPIL_ERR_INVALID, "null argument");
+    if (std::memcmp(pt->sc.camera.s2c, sample_to_camera, sizeof(pt->sc.camera.s2c)) != 0 ||
+        std::memcmp(pt->sc.camera.c2w, camera_to_world, sizeof(pt->sc.camera.c2w)) != 0)
+        pt->ahead_valid = false;  // the render-ahead camera rays belong to the old view
     std::memcpy(pt->sc.camera.s2c, sample_to_camera, sizeof(pt->sc.camera.s2c));
     std::memcpy(pt->sc.camera.c2w, camera_to_world, sizeof(pt->sc.camera.c2w));
     return PUPIL_OK;
@@ -643,6 +658,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     if (instance >= pt->h_insts.size()) return fail(PUPIL_ERR_INVALID, "instance index out of range");
     HIP_TRY(hipSetDevice(pt->device));
     HIP_TRY(hipDeviceSynchronize());  // no render may still read the old tables
+    pt->ahead_valid = false;          // render-ahead hits were traced against the old geometry
     DevInstance &d = pt->h_insts[instance];
     std::memcpy(d.to_world, to_world, sizeof(d.to_world));
     std::memcpy(d.to_object, to_object, sizeof(d.to_object));
@@ -704,6 +720,7 @@ int pupil_pt_update_emitters(pupil_pt *pt, const pupil_scene_desc *scene) {
     if (scene->num_area_emitters && !scene->area_emitters) return fail(PUPIL_ERR_INVALID, "missing emitter array");
     HIP_TRY(hipSetDevice(pt->device));
     HIP_TRY(hipDeviceSynchronize());
+    pt->ahead_valid = false;
     return upload_emitters(pt, scene);
 }
 
@@ -742,8 +759,32 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     if (num_local == 0) return PUPIL_OK;
     const size_t paths = (size_t)num_local * launch->spp;
     if (paths >= (1ull << 31)) return fail(PUPIL_ERR_UNSUPPORTED, "too many paths in one batch");
-    int rc = ensure_state(pt, paths);
+    const bool stats = (launch->collect_stats & PUPIL_STATS_COUNTERS) != 0;
+    const bool timing = (launch->collect_stats & PUPIL_STATS_TIMING) != 0;
+    const uint32_t depth = launch->max_depth ? launch->max_depth : pt->max_depth;
+    // render-ahead: use the camera rays the previous render traced for this one, and
+    // trace the next render's in this one's last mixed launch (BVH4 persistent kernels;
+    // counter renders keep their own primary launch so the counters stay per render)
+    const bool use_ahead = pt->ahead_valid && !stats && launch->random_seed == pt->ahead_seed && launch->spp == pt->ahead_spp &&
+                           num_local == pt->ahead_local && std::memcmp(key, pt->ahead_key, sizeof(key)) == 0;
+    const bool make_ahead = pt->ahead_mode != 0 && (pt->ahead_mode == 2 || launch->spp == 1) && !stats &&
+                            depth >= 2 && pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill != 0 &&
+                            paths < (1ull << 30);
+    pt->ahead_valid = false;
+    if (pt->last_stream && s != pt->last_stream) HIP_TRY(hipStreamWaitEvent(s, pt->ev_end, 0));
+    const size_t cap_before = pt->cap;
+    int rc = ensure_state(pt, paths * (use_ahead || make_ahead ? 2 : 1));
     if (rc) return rc;
+    const uint32_t half = use_ahead && pt->cap == cap_before ? pt->ahead_half : 0u;
+    const bool ahead_in = use_ahead && pt->cap == cap_before;
+    auto view = [&](uint32_t h) {  // path state of half h: every array offset by h * paths
+        PathState v = pt->ps;
+        const size_t o = (size_t)h * paths;
+        v.ray_o += o, v.ray_d += o, v.hit += o, v.thr += o, v.rad += o, v.misc += o;
+        v.sh_o += o, v.sh_d += o, v.sh_c += o, v.mbin += o, v.sflags += o;
+        return v;
+    };
+    const PathState ps = view(half);
 
     FrameParams fp{};
     fp.width = pt->width;
@@ -762,8 +803,6 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     fp.albedo = (float *)out->albedo;
     fp.normal = (float *)out->normal;
     fp.test = (float *)out->test;
-    const bool stats = (launch->collect_stats & PUPIL_STATS_COUNTERS) != 0;
-    const bool timing = (launch->collect_stats & PUPIL_STATS_TIMING) != 0;
     fp.nee_count = stats ? pt->trace_counters + 16 : nullptr;
 
     TraceStats ts_dev{pt->trace_counters};
@@ -807,55 +846,78 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     Queues &q = pt->q;
     // material bins of the traced paths -> q.bins (stable, increasing path id)
     auto bin_paths = [&]() {
-        launch_partition(pt->ps.mbin, np, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
+        launch_partition(ps.mbin, np, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
                          q.counts + kStartBins, q.counts + kScratch, nullptr, s);
     };
     // No per-stage clears: the primary extend writes every path's material bin,
     // each shade writes its paths' flags (with the bounce tag) and resets their
     // bin to 0xFF, the persistent kernels reset their own work heads, and the
     // flags partition logs the per-bounce ray counts.
-    launch_generate(pt->sc, fp, pt->ps, s);
-    ev0(0);
-    tail_slot();
-    // camera rays: the spp samples of a pixel on consecutive lanes (PUPIL_PRIMARY_ORDER=path: path order)
-    launch_extend(pt->sc, pt->ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s,
-                  pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u, fp.num_local);
-    ev1();
+    const uint32_t interleave = pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u;
+    if (!ahead_in) {  // else the previous render traced this one's camera rays (render-ahead)
+        launch_generate(pt->sc, fp, ps, s);
+        ev0(0);
+        tail_slot();
+        // camera rays: the spp samples of a pixel on consecutive lanes (PUPIL_PRIMARY_ORDER=path: path order)
+        launch_extend(pt->sc, ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s, interleave, fp.num_local);
+        ev1();
+    }
     if (!pt->shade_list) bin_paths();
     for (uint32_t b = 0; b < bounces; b++) {
         const uint32_t tag = sflag_tag(fp.max_depth, b);
-        if (tag == 0) HIP_TRY(hipMemsetAsync(pt->ps.sflags, 0, np, s));
+        if (tag == 0) HIP_TRY(hipMemsetAsync(ps.sflags, 0, np, s));
         ev0(2);
-        launch_shade(pt->sc, fp, pt->ps, q, b, s, !pt->shade_list ? kShadeBins : (b == 0 ? kShadeAll : kShadeNext));
+        launch_shade(pt->sc, fp, ps, q, b, s, !pt->shade_list ? kShadeBins : (b == 0 ? kShadeAll : kShadeNext));
         ev1();
         if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
             // next (bit 0) and shadow (bit 1) lists -> q.nxsh, each in increasing path order
             // (grouping the next list by direction octant measured slower: 21.2 vs 20.8 ms extend)
-            launch_partition(pt->ps.sflags, np, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
+            launch_partition(ps.sflags, np, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
                              q.counts + kStartNext, nullptr, b < 128 ? pt->ray_log + 2 * b : nullptr, s);
             if (pt->mixed_trace && pt->sc.bvh_width >= 4 && pt->sc.trace_refill) {
+                // render-ahead: the last mixed launch also traces the next render's camera rays,
+                // generated into the other half of the buffers (seed + spp, this camera and tiling)
+                const bool ahead_out = make_ahead && b + 2 == bounces;
+                if (ahead_out) {
+                    FrameParams fa = fp;
+                    fa.seed0 = fp.seed0 + fp.spp;
+                    launch_generate(pt->sc, fa, view(half ^ 1u), s);
+                }
                 ev0(1);
                 tail_slot();
-                launch_trace_mixed(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);
+                if (ahead_out)  // addressed from the base of both halves (offsets stay non-negative)
+                    launch_trace_mixed(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s, np, half * np,
+                                       (half ^ 1u) * np, interleave, fp.num_local);
+                else
+                    launch_trace_mixed(pt->sc, ps, q, pt->ovf, pt->ovf_threads, tsp, s);
                 ev1();
+                if (ahead_out) {
+                    pt->ahead_valid = true;
+                    pt->ahead_seed = fp.seed0 + fp.spp;
+                    pt->ahead_spp = fp.spp;
+                    pt->ahead_local = num_local;
+                    pt->ahead_half = half ^ 1u;
+                    std::memcpy(pt->ahead_key, key, sizeof(key));
+                }
             } else {
                 ev0(1);
-                launch_shadow(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s);
+                launch_shadow(pt->sc, ps, q, pt->ovf, pt->ovf_threads, tsp, s);
                 ev1();
                 ev0(0);
-                launch_extend(pt->sc, pt->ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, tsp, s);
+                launch_extend(pt->sc, ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, tsp, s);
                 ev1();
             }
             if (!pt->shade_list) bin_paths();
         }
     }
-    launch_accumulate(fp, pt->ps, s);
+    launch_accumulate(fp, ps, s);
     HIP_TRY(hipEventRecord(pt->ev_end, s));
     HIP_TRY(hipGetLastError());
     pt->trace_pairs = pair;
     pt->last_paths = fp.num_paths;
     pt->last_bounces = bounces < 129 ? bounces : 129;  // rays are logged for bounces 0..127
     pt->last_stats = stats;
+    pt->last_stream = s;
     return PUPIL_OK;
 }
 

@@ -130,8 +130,14 @@ void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState 
 void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                    const TraceStats *stats, hipStream_t s);
 // one persistent launch over the next + shadow lists of a bounce (BVH4 persistent path only)
+// ahead_count > 0 (render-ahead, BVH4 kernels only): the launch also traces the camera
+// rays of the next render.  `ps` is then the base of both buffer halves: this render's
+// listed paths are at list_base + id, the next render's camera rays (generated there)
+// at ahead_base + [0, ahead_count), dequeued pixel-major when ahead_spp > 1 (as the
+// primary extend)
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
-                        const TraceStats *stats, hipStream_t s);
+                        const TraceStats *stats, hipStream_t s, uint32_t ahead_count = 0, uint32_t list_base = 0,
+                        uint32_t ahead_base = 0, uint32_t ahead_spp = 0, uint32_t ahead_local = 0);
 void launch_accumulate(const FrameParams &fp, const PathState &ps, hipStream_t s);
 uint32_t trace_grid_blocks();
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,

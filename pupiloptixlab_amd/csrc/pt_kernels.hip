@@ -478,7 +478,9 @@ __device__ __forceinline__ void csel(float &ta, int &la, float &tb, int &lb) {
 // kModeMixed: one launch over the concatenated next + shadow lists of a bounce
 // (q.nxsh[0, cnt_next) extension rays, then cnt_shadow shadow rays), so each
 // bounce pays one persistent-kernel tail instead of two.
-enum TraceMode : int { kModeExtend = 0, kModeShadow = 1, kModeRays = 2, kModeMixed = 3 };
+// kModeMixedAhead: kModeMixed plus the next render's camera rays (render-ahead,
+// TraceJob::ahead_off); a separate instance so the plain mixed kernel keeps its registers
+enum TraceMode : int { kModeExtend = 0, kModeShadow = 1, kModeRays = 2, kModeMixed = 3, kModeMixedAhead = 4 };
 
 struct TraceJob {
     const uint32_t *queue;      // extend: path ids (null = identity)
@@ -494,6 +496,12 @@ struct TraceJob {
     // path ids stay sample major; spp = 0: identity
     uint32_t spp;
     uint32_t num_local;
+    // kModeMixedAhead (render-ahead, engine.hip): static_count camera rays of the next render
+    // ride along; the path state passed is the base of both halves of the buffers, list path
+    // ids are offset by list_base (this render's half), ahead position j -> path (pixel-major
+    // as above) + ahead_base (the other half); both offsets are non-negative
+    uint32_t list_base;
+    uint32_t ahead_base;
 };
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
@@ -602,10 +610,13 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                                             const TraceJob &job, int *ovf, uint32_t ovf_threads,
                                             const TraceStats &stats, int *s_ring) {
     constexpr float kInf = __builtin_huge_valf();
-    const uint32_t n_next = MODE == kModeMixed ? q.counts[kCntNext] : 0u;
+    constexpr bool kMixed = MODE == kModeMixed || MODE == kModeMixedAhead;
+    const uint32_t n_next = kMixed ? q.counts[kCntNext] : 0u;
+    // mixed launches may carry the next render's camera rays (render-ahead, TraceJob::ahead_off)
+    const uint32_t n_ahead = MODE == kModeMixedAhead ? job.static_count : 0u;
     const uint32_t count =
         MODE == kModeShadow ? q.counts[kCntShadow]
-                            : (MODE == kModeMixed ? n_next + q.counts[kCntShadow]
+                            : (kMixed ? n_next + q.counts[kCntShadow]
                                                   : (job.count_ptr ? *job.count_ptr : job.static_count));
     const uint32_t *shadow_q = MODE == kModeShadow ? q.nxsh + q.counts[kStartShadow] : nullptr;
     RingStack st;
@@ -648,13 +659,18 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             // extension and the shadow list separately and give each chunk its
             // extension share first, so every chunk ends on (cheaper) shadow rays
             // and the launch tail is not made of closest-hit traversals.
-            uint32_t lo, len, len_e = 0, lo_s = 0;
-            if (MODE == kModeMixed) {
+            uint32_t lo, len, len_e = 0, lo_s = 0, lo_a = 0, len_a = 0;
+            if (kMixed) {
+                // chunk = its share of the render-ahead camera rays (kModeMixedAhead only:
+                // coherent, traced first as in a primary launch, whose tail the bounce
+                // rays then fill), of the extension list, then of the shadow list
                 const uint32_t n_sh = count - n_next;
                 lo = (uint32_t)((uint64_t)n_next * shard / kWorkShards);
                 len_e = (uint32_t)((uint64_t)n_next * (shard + 1) / kWorkShards) - lo;
+                lo_a = (uint32_t)((uint64_t)n_ahead * shard / kWorkShards);
+                len_a = (uint32_t)((uint64_t)n_ahead * (shard + 1) / kWorkShards) - lo_a;
                 lo_s = n_next + (uint32_t)((uint64_t)n_sh * shard / kWorkShards);
-                len = len_e + (n_next + (uint32_t)((uint64_t)n_sh * (shard + 1) / kWorkShards) - lo_s);
+                len = len_e + len_a + (n_next + (uint32_t)((uint64_t)n_sh * (shard + 1) / kWorkShards) - lo_s);
             } else {
                 lo = (uint32_t)((uint64_t)count * shard / kWorkShards);
                 len = (uint32_t)((uint64_t)count * (shard + 1) / kWorkShards) - lo;
@@ -676,7 +692,8 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             }
             if (!active) {
                 const uint32_t k = base + (uint32_t)__popcll(idle & lanemask_lt());
-                const uint32_t i = MODE == kModeMixed && k >= len_e ? lo_s + (k - len_e) : lo + k;
+                const uint32_t ke = k - len_a;  // past the render-ahead share (len_a = 0 outside kModeMixedAhead)
+                const uint32_t i = kMixed && ke >= len_e ? lo_s + (ke - len_e) : lo + ke;
                 if (k < len) {
                     float4 o, d;
                     if (MODE == kModeExtend) {
@@ -691,8 +708,18 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         d = ps.sh_d[p];
                         tmin = 0.001f;
                         tmax = o.w;
-                    } else if (MODE == kModeMixed) {
-                        p = q.nxsh[i];
+                    } else if (MODE == kModeMixedAhead && k < len_a) {
+                        // a camera ray of the next render (generated into the other half of the
+                        // path state): the primary extend's pixel-major dequeue, then the offset
+                        const uint32_t j = lo_a + k;
+                        p = (job.spp ? (j % job.spp) * job.num_local + j / job.spp : j) + job.ahead_base;
+                        any = false;
+                        o = ps.ray_o[p];
+                        d = ps.ray_d[p];
+                        tmin = 0.001f;
+                        tmax = kMaxDistance;
+                    } else if (kMixed) {
+                        p = q.nxsh[i] + (MODE == kModeMixedAhead ? job.list_base : 0u);
                         any = i >= n_next;
                         o = any ? ps.sh_o[p] : ps.ray_o[p];
                         d = any ? ps.sh_d[p] : ps.ray_d[p];
@@ -737,7 +764,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             while ((uint32_t)node < (uint32_t)kSentinel) {
                 const Bvh4Node n = sc.nodes4[node];
                 if (STATS) {
-                    if (MODE == kModeMixed && any) nv_sh++;
+                    if (kMixed && any) nv_sh++;
                     else nv++;
                     const unsigned long long m = __ballot(true);
                     if ((int)lane_id() == __ffsll((long long)m) - 1) {
@@ -781,7 +808,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         dg[3] += (unsigned long long)__popcll(m);
                     }
                 }
-                uint32_t &np_cnt = MODE == kModeMixed && any ? npt_sh : npt;
+                uint32_t &np_cnt = kMixed && any ? npt_sh : npt;
                 if (TL && !in_blas) {  // a TLAS leaf: one instance
                     const uint32_t id = leaf_first(leaf);
                     const DevInstance &in = sc.instances[id];
@@ -840,7 +867,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         }
         const bool done = active && ((node == kSentinel && leaf >= 0) || (any && found));
         // ---- retire
-        if (MODE == kModeExtend || MODE == kModeMixed) {
+        if (MODE == kModeExtend || kMixed) {
             uint32_t bin = 0;
             if (done && !any) {
                 // hit index: the record (flat) or the global primitive id (two-level shading,
@@ -858,7 +885,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 ps.mbin[p] = (uint8_t)bin;  // material bin for the partition
             }
         }
-        if (MODE == kModeShadow || MODE == kModeMixed) {
+        if (MODE == kModeShadow || kMixed) {
             if (done && any && !found) {  // main.cu:124-139
                 const float4 c = ps.sh_c[p];
                 float4 L = ps.rad[p];
@@ -877,7 +904,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         if (done) active = false;
     }
     flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
-    if (MODE == kModeMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
+    if (kMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
     flush_stats<STATS>(&stats, n_unique, 0u, 18);
     if (STATS && stats.wave_times && lane_id() == 0) {
         unsigned long long *w = stats.wave_times + 4ull * (blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u);
@@ -1755,12 +1782,15 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
     const TraceStats st = stats ? *stats : TraceStats{nullptr};
     const uint32_t blocks = trace4_blocks(sc, ovf_threads);
     if (sc.bvh_width == 8) {
-        if (stats)
+        if constexpr (MODE == kModeMixedAhead) {
+            return;  // the engine keeps render-ahead to BVH4 trees
+        } else if (stats) {
             hipLaunchKernelGGL((k_trace8<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
                                ovf_threads, st);
-        else
+        } else {
             hipLaunchKernelGGL((k_trace8<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
                                ovf_threads, st);
+        }
     } else if (sc.two_level && !sc.tl_world) {
         if (stats)
             hipLaunchKernelGGL((k_trace4tl<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
@@ -1880,9 +1910,13 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
 }
 
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
-                        const TraceStats *stats, hipStream_t s) {
-    const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min, nullptr, nullptr, 0u, 0u};
-    launch_trace4<kModeMixed, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
+                        const TraceStats *stats, hipStream_t s, uint32_t ahead_count, uint32_t list_base,
+                        uint32_t ahead_base, uint32_t ahead_spp, uint32_t ahead_local) {
+    const TraceJob job{nullptr,       nullptr,   ahead_count,          q.work + kWorkExtend,
+                       sc.trace_refill, sc.trace_node_min, nullptr, nullptr,
+                       ahead_count ? ahead_spp : 0u, ahead_local, list_base, ahead_base};
+    if (ahead_count) launch_trace4<kModeMixedAhead, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
+    else launch_trace4<kModeMixed, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
 }
 
 // Shade launch size: one thread per path of the batch (fp.num_paths bounds the

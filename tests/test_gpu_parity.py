@@ -505,6 +505,67 @@ def test_camera_change_uploads_new_sensor():
     assert np.array_equal(moved.view(np.uint32), ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("case", ["flat", "two_level", "bins", "batched"])
+def test_render_ahead_onrun_sequence(case, monkeypatch):
+    """Render-ahead (engine.hip, PUPIL_AHEAD): the last mixed launch of an OnRun traces
+    the camera rays of the next OnRun.  A sequence of OnRuns on one engine must equal
+    the oracle after every frame, including when the camera moves (the traced-ahead
+    rays belong to the old view), when the seed jumps (they belong to another frame),
+    after an instance update, and for max_depth 1 (no mixed launch to ride in)."""
+    import torch
+    from pupiloptixlab_amd.pt_pass import PTPass, Events
+    from pupiloptixlab_amd import world as W
+
+    if case == "two_level":
+        monkeypatch.setenv("PUPIL_ACCEL", "two_level")
+        monkeypatch.setenv("PUPIL_TL_MODE", "object")
+    if case == "batched":
+        monkeypatch.setenv("PUPIL_AHEAD", "2")
+    if case == "bins":
+        w = World().load_scene(scenes.cornell_materials_xml(os.path.join(TMP, "cbmat48.xml"), 48, 40, 5))
+    elif case == "two_level":
+        w = scenes.instanced_field(num_instances=6, width=48, height=32, max_depth=5, seed=2, spheres_per_blas=8)
+    elif case == "flat":
+        w = scenes.sphere_field(8, 48, 32, 4, seed=5, merge=False)
+    else:
+        w = _cornell(48)
+    spp = 2 if case == "batched" else 1
+    pt = PTPass(device=0)
+    pt.set_scene(w)
+
+    def step(k_frames, o, seed0=0, depth=0):
+        pt.render(spp)
+        torch.cuda.synchronize()
+        got = pt.buffers.get("pt accum buffer").cpu().numpy()
+        ref = o.render(spp=k_frames * spp, random_seed=seed0, max_depth=depth)["accum"]
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (case, k_frames, seed0)
+
+    o = oracle.OracleScene(w.desc())
+    for k in range(1, 4):
+        step(k, o)
+    if case in ("flat", "batched"):  # the camera moves: accumulation restarts on the new view
+        w.set_sensor(40.0, W.look_at_mitsuba((0.3, 1.2, 3.5), (0.0, 0.9, 0.0), (0.0, 1.0, 0.0)), fov_axis="x")
+        pt.events.dispatch(Events.CAMERA_CHANGE)
+        o = oracle.OracleScene(w.desc())
+        for k in range(1, 3):
+            step(k, o)
+    if case in ("flat", "two_level"):  # an instance moves: the rays traced ahead hit the old geometry
+        w.set_instance_transform(1, W.transform(scale=(1.5, 1.5, 1.5), rotate=((0, 1, 0), 30), translate=(0.5, 1.0, -0.5)))
+        pt.update_instance(w, 1)
+        o = oracle.OracleScene(w.desc())
+        for k in range(1, 3):
+            step(k, o)
+    # the seed jumps: the rays traced ahead for the next seed are not used
+    pt.random_seed, pt.sample_cnt = 9, 0
+    step(1, o, seed0=9)
+    # max_depth 1: no mixed launch, so no render-ahead; the next render still matches
+    pt.max_depth = 1
+    pt.random_seed, pt.sample_cnt = 0, 0
+    step(1, o, depth=1)
+    step(2, o, depth=1)
+    pt.close_engine()
+
+
 @pytest.mark.parametrize("accel", ["flat", "two_level"])
 def test_skewed_scene_stays_within_stack_capacity(accel, monkeypatch):
     """A geometric chain of triangles (size and spacing x1.15 per triangle) makes the
