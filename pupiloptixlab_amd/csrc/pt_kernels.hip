@@ -159,6 +159,11 @@ __device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const 
     for (uint32_t i = first; i < first + count; i++) {
         const float4 a = sc.prims[3 * i + 0];
         const float4 b = sc.prims[3 * i + 1];
+        const float4 c = sc.prims[3 * i + 2];
+        // the whole 48-B record in one round trip: without this the compiler sinks the
+        // vertex loads below the sphere-bit branch, a second dependent fetch per record
+        asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(c.x),
+                     "v"(c.y), "v"(c.z));
         const uint32_t ref = __float_as_uint(a.w);
         const uint32_t key = ref & ~kPrimSphereBit;
         if (STATS) prims_tested++;
@@ -168,7 +173,6 @@ __device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const 
             const DevInstance &in = sc.instances[__float_as_uint(b.w)];
             hit = intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, t);
         } else {
-            const float4 c = sc.prims[3 * i + 2];
             hit = intersect_triangle(r, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), tmin, tmax, t, b1,
                                      b2);
         }
