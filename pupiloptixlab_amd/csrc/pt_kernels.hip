@@ -1392,18 +1392,29 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, v
     uint32_t inst_id, gprim;
     bool sphere;
     const float4 *rec;
+    float4 ra[7];  // the shading record (one 128-B line)
     if (sc.two_level) {
         gprim = idx;
         inst_id = sc.prim_inst[idx];
         const DevInstance &ti = sc.instances[inst_id];
         sphere = ti.kind == PUPIL_SHAPE_SPHERE;
         rec = sc.attrs + (size_t)kAttrStride * (sphere ? 0u : ti.attr_base + (idx - ti.prim_offset));
+        for (int k = 0; k < 7; k++) ra[k] = rec[k];
     } else {
         rec = sc.attrs + (size_t)kAttrStride * idx;
-        const uint32_t ref = __float_as_uint(rec[0].w);
+        // the whole line in one round trip, with the instance: without the barrier the
+        // compiler sinks the normal / texcoord loads below the instance's flags, a second
+        // dependent fetch per hit
+        for (int k = 0; k < 7; k++) ra[k] = rec[k];
+        asm volatile("" ::"v"(ra[0].x), "v"(ra[0].y), "v"(ra[0].z), "v"(ra[0].w), "v"(ra[1].x), "v"(ra[1].y),
+                     "v"(ra[1].z), "v"(ra[1].w), "v"(ra[2].x), "v"(ra[2].y), "v"(ra[2].z), "v"(ra[2].w), "v"(ra[3].x),
+                     "v"(ra[3].y));
+        asm volatile("" ::"v"(ra[3].z), "v"(ra[3].w), "v"(ra[4].x), "v"(ra[4].y), "v"(ra[4].z), "v"(ra[4].w),
+                     "v"(ra[5].x), "v"(ra[5].y), "v"(ra[5].z), "v"(ra[5].w), "v"(ra[6].x), "v"(ra[6].y));
+        const uint32_t ref = __float_as_uint(ra[0].w);
         gprim = ref & ~kPrimSphereBit;
         sphere = (ref & kPrimSphereBit) != 0u;
-        inst_id = __float_as_uint(rec[1].w);
+        inst_id = __float_as_uint(ra[1].w);
     }
     const DevInstance &in = sc.instances[inst_id];
     out.inst = inst_id;
@@ -1418,9 +1429,9 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, v
         if (in.flip_normals) g.normal = g.normal * -1.f;
     } else {
         local = gprim - in.prim_offset;
-        const float4 a = rec[0];
-        const float4 b = rec[1];
-        const float4 c = rec[2];
+        const float4 a = ra[0];
+        const float4 b = ra[1];
+        const float4 c = ra[2];
         const vec3 p0 = v3(a.x, a.y, a.z);
         const vec3 p1 = v3(b.x, b.y, b.z);
         const vec3 p2 = v3(c.x, c.y, c.z);
@@ -1430,7 +1441,7 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, v
         g.position = xform_point(in.to_world, g.position);
         vec3 n;
         if (in.normals) {
-            const float4 d = rec[3], e = rec[4];
+            const float4 d = ra[3], e = ra[4];
             const vec3 n0 = v3(c.w, d.x, d.y);
             const vec3 n1 = v3(d.z, d.w, e.x);
             const vec3 n2 = v3(e.y, e.z, e.w);
@@ -1441,7 +1452,7 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, v
         g.normal = normalize(xform_normal(in.to_object, n));
         if (in.flip_normals) g.normal = g.normal * -1.f;
         if (in.texcoords) {
-            const float4 t01 = rec[5], t2 = rec[6];
+            const float4 t01 = ra[5], t2 = ra[6];
             const vec2 t0 = v2(t01.x, t01.y);
             const vec2 t1 = v2(t01.z, t01.w);
             const vec2 tt2 = v2(t2.x, t2.y);
