@@ -606,6 +606,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
             if (std::strcmp(sl, "bins") == 0) pt->shade_list = false;
             if (std::strcmp(sl, "list") == 0) pt->shade_list = true;
         }
+        sc.single_bin = pt->shade_list && bins && (bins & (bins - 1u)) == 0u ? (uint32_t)__builtin_ctz(bins) : 0u;
     }
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;

@@ -878,7 +878,9 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 // reconstruct(); the world-mode flat kernel keeps it in best_key)
                 const uint32_t hidx = !TL && sc.two_level ? best_key : best_idx;
                 ps.hit[p] = make_float4(found ? tmax : -1.f, b1, b2, __uint_as_float(found ? hidx : kMissIndex));
-                if (found) {
+                // single-material scenes: shading reads the bin off the hit (no dependent
+                // record fetch here, which would stall the wave before its next refill)
+                if (found && sc.single_bin == 0u) {
                     if (TL) {
                         bin = sc.instances[sc.prim_inst[best_idx]].bin;
                     } else {
@@ -886,7 +888,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
                     }
                 }
-                ps.mbin[p] = (uint8_t)bin;  // material bin for the partition
+                if (sc.single_bin == 0u) ps.mbin[p] = (uint8_t)bin;  // material bin for the partition
             }
         }
         if (MODE == kModeShadow || kMixed) {
@@ -1683,6 +1685,8 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, Frame
         if (LIST == kShadeBins) {
 #pragma unroll
             for (int b = 1; b < kPartMaxBins; b++) bin = i >= start[b] ? (uint32_t)b : bin;
+        } else if (sc.single_bin) {  // the traversal wrote no bin byte (DeviceScene::single_bin)
+            bin = __float_as_uint(ps.hit[p].w) == kMissIndex ? 0u : sc.single_bin;
         } else {
             bin = ps.mbin[p];
         }
@@ -1704,7 +1708,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, Frame
                 atomicAdd(fp.nee_count, (unsigned long long)__popcll(m));
         }
         ps.sflags[p] = (uint8_t)((flags & 3u) | tag << 2);
-        ps.mbin[p] = 0xFFu;  // listed again only if the next extend traces this path
+        if (LIST == kShadeBins) ps.mbin[p] = 0xFFu;  // listed again only if the next extend traces this path
     }
 }
 

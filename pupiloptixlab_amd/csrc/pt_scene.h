@@ -165,6 +165,9 @@ struct DeviceScene {
     uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
     uint32_t num_cus;       // compute units of the device (persistent grid size)
     uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node
+    // every instance has this material bin (1..8; 0 = several): shading then derives a
+    // path's bin from its hit record and the persistent traversal writes no bin byte
+    uint32_t single_bin;
     uint32_t tl_world;        // two-level "world" mode: nodes4 = braided TLAS + world-space BLAS copies,
                               // prims = flat-format world records; traversed by the flat kernels
     uint32_t two_level;       // 1: nodes4 = TLAS over instances + object-space BLAS per shape;
