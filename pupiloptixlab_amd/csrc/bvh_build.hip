@@ -336,14 +336,14 @@ __global__ void k_emit(int n, const uint32_t *sorted_vals, const Aabb *prim_boxe
 // ---------------------------------------------------------------- PLOC
 // Parallel locally-ordered clustering (Meister & Bittner 2018) over the
 // Morton-ordered primitives: each cluster finds its nearest neighbour (smallest
-// union surface area, ties to the smaller index) within +-kPlocRadius
+// union surface area, ties to the smaller index) within +-kPlocRadius (32: 2.5 % faster frames than 16 on config 4, 64 no better; profiles/r02_ploc_radius_ab.txt)
 // positions, mutual pairs merge, the cluster list is compacted in order, and
 // this repeats until one cluster is left.  It yields a tree of markedly lower
 // SAH cost than the Karras hierarchy over the same order.  The result is
 // converted to the LBVH arrays (children / ranges / parents / node boxes, root
 // 0, subtrees contiguous in a new primitive order) so emit and the BVH4
 // collapse are shared.  Refs: >= 0 internal node (creation id), < 0 leaf ~pos.
-constexpr int kPlocRadius = 16;
+constexpr int kPlocRadius = 32;
 constexpr int kScanBlock = 1024;
 constexpr int kScanItems = 4;
 
