@@ -703,6 +703,135 @@ __global__ void k_collapse_emit(int items, int base, int next_base, const int *i
     nodes4[base + t] = o;
 }
 
+// ---------------------------------------------------------------- SAH-optimal BVH4 collapse
+// (the default; PUPIL_BVH4_COLLAPSE=greedy keeps the greedy opening) The slot distribution of Ylitie, Karras & Laine 2017,
+// section 4, for 4-wide nodes: bottom up over the binary tree, C(n, i) is the least
+// cost of the subtree n when it may fill i slots of its parent, with
+//   D(n, j)  = min over 0 < k < j of C(left, k) + C(right, j - k)
+//   C(n, 1)  = A(n) + D(n, 4)            (n becomes a 4-wide node)
+//   C(n, i)  = min(C(n, i - 1), D(n, i)) (n opened into up to i slots)
+// Subtrees of at most leaf_size primitives are leaves, as in the greedy collapse, so
+// their cost is the same in every distribution and only the surface area of the
+// 4-wide nodes is minimised.  dec[n]: bits 0-1 / 2-3 / 4-5 the best k of D(n, 2/3/4),
+// bits 8-10 "C(n, i) = C(n, i - 1)" for i = 2, 3, 4.
+__global__ void k_sah_parents(int n, const int2 *children, int *parent, int *leaf_parent) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n - 1) return;
+    const int2 c = children[b];
+    if (c.x >= 0) parent[c.x] = b;
+    else leaf_parent[~c.x] = b;
+    if (c.y >= 0) parent[c.y] = b;
+    else leaf_parent[~c.y] = b;
+}
+
+__device__ __forceinline__ float4 sah_cost(int c, const float4 *cost, const uint32_t *sorted_vals,
+                                           const Aabb *prim_boxes) {
+    if (c < 0) {  // one primitive: a leaf in every distribution
+        const float a = half_area(prim_boxes[sorted_vals[~c]]);
+        return make_float4(a, a, a, a);
+    }
+    const uint32_t *w = (const uint32_t *)(cost + c);  // written by another thread: device-coherent loads
+    float4 v;
+    v.x = __uint_as_float(__hip_atomic_load(w + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    v.y = __uint_as_float(__hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    v.z = __uint_as_float(__hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    v.w = __uint_as_float(__hip_atomic_load(w + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return v;
+}
+
+// one thread per primitive walks up; the second child to finish computes its parent
+__global__ void k_sah_dp(int n, const int *parent, const int *leaf_parent, const int2 *children, const int2 *ranges,
+                         const Aabb *node_boxes, const uint32_t *sorted_vals, const Aabb *prim_boxes,
+                         uint32_t leaf_size, uint32_t *flags, float4 *cost, uint32_t *dec) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int b = leaf_parent[i];
+    while (b >= 0) {
+        __threadfence();
+        if (atomicAdd(flags + b, 1u) == 0u) return;
+        __threadfence();
+        const int2 ch = children[b];
+        const float4 l4 = sah_cost(ch.x, cost, sorted_vals, prim_boxes);
+        const float4 r4 = sah_cost(ch.y, cost, sorted_vals, prim_boxes);
+        const float cl[4] = {l4.x, l4.y, l4.z, l4.w}, cr[4] = {r4.x, r4.y, r4.z, r4.w};
+        float d[5];
+        uint32_t code = 0;
+        for (int j = 2; j <= 4; j++) {
+            float best = __builtin_huge_valf();
+            uint32_t bk = 1;
+            for (int k = 1; k < j; k++) {
+                const float v = cl[k - 1] + cr[j - k - 1];
+                if (v < best) {
+                    best = v;
+                    bk = (uint32_t)k;
+                }
+            }
+            d[j] = best;
+            code |= bk << (2 * (j - 2));
+        }
+        const int2 r = ranges[b];
+        const float a = half_area(node_boxes[b]);
+        float c4[4];
+        if ((uint32_t)(r.y - r.x + 1) <= leaf_size) {  // a leaf wherever it goes
+            c4[0] = c4[1] = c4[2] = c4[3] = a * (float)(r.y - r.x + 1);
+            code |= 7u << 8;
+        } else {
+            c4[0] = a + d[4];
+            for (int s = 2; s <= 4; s++) {
+                if (c4[s - 2] <= d[s]) {
+                    c4[s - 1] = c4[s - 2];
+                    code |= 1u << (8 + s - 2);
+                } else {
+                    c4[s - 1] = d[s];
+                }
+            }
+        }
+        cost[b] = make_float4(c4[0], c4[1], c4[2], c4[3]);
+        dec[b] = code;
+        b = parent[b];
+    }
+}
+
+// children of the 4-wide node made from binary node b: D(b, 4) distributed down the
+// decisions, a subtree taking one slot (a leaf or the next level's 4-wide node) or
+// being opened into the slots it was given
+__global__ void k_collapse_pick_sah(int items, const int *item_node, const int2 *children, const int2 *ranges,
+                                    const uint32_t *dec, uint32_t leaf_size, int4 *clist,
+                                    unsigned long long *inner_count) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= items) return;
+    const int b = item_node[t];
+    const int2 ch = children[b];
+    const uint32_t k4 = (dec[b] >> 4) & 3u;
+    int wc[4], wi[4], nw = 0;  // work: (subtree, slots); slots add up to at most 4
+    wc[nw] = ch.x, wi[nw++] = (int)k4;
+    wc[nw] = ch.y, wi[nw++] = 4 - (int)k4;
+    int c[4], nk = 0;
+    while (nw > 0) {
+        const int x = wc[--nw];
+        int s = wi[nw];
+        if (!opens(x, ranges, leaf_size) || s <= 1) {
+            c[nk++] = x;
+            continue;
+        }
+        const uint32_t dx = dec[x];
+        while (s > 1 && ((dx >> (8 + s - 2)) & 1u)) s--;  // C(x, s) = C(x, s - 1)
+        if (s == 1) {
+            c[nk++] = x;
+            continue;
+        }
+        const int k = (int)((dx >> (2 * (s - 2))) & 3u);
+        const int2 g = children[x];
+        wc[nw] = g.x, wi[nw++] = k;
+        wc[nw] = g.y, wi[nw++] = s - k;
+    }
+    unsigned long long inner = 0;
+    for (int k = 0; k < nk; k++) inner += opens(c[k], ranges, leaf_size) ? 1ull : 0ull;
+    for (int k = nk; k < 4; k++) c[k] = kEmptyLink;
+    clist[t] = make_int4(c[0], c[1], c[2], c[3]);
+    inner_count[t] = inner;
+}
+
 // ---------------------------------------------------------------- greedy BVH8 collapse
 // Same greedy surface-area opening as the BVH4 collapse, up to eight children.
 // Each child then gets the slot whose octant best matches its centroid offset
@@ -900,8 +1029,14 @@ hipError_t dmalloc(T **p, size_t count) {
 // nodes4 must hold n - 1 entries; returns the number of 4-wide nodes.
 hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
                          const int2 *ranges, const Aabb *node_boxes, uint32_t leaf_size, Bvh4Node *nodes4,
-                         uint32_t *num_nodes4, uint32_t *depth4, std::vector<uint32_t> *level_start, hipStream_t s) {
+                         uint32_t *num_nodes4, uint32_t *depth4, std::vector<uint32_t> *level_start, hipStream_t s,
+                         bool sah) {
     int *items_a = nullptr, *items_b = nullptr;
+    // SAH-optimal slot distribution (k_sah_dp) instead of the greedy opening
+    int *parent = nullptr, *leaf_parent = nullptr;
+    uint32_t *sflags = nullptr, *dec = nullptr;
+    float4 *cost = nullptr;
+    sah = sah && n >= 2;
     int4 *clist = nullptr;
     unsigned long long *cnt = nullptr, *sums = nullptr, *total = nullptr;
     const int per = kScanBlock * kScanItems;
@@ -912,15 +1047,33 @@ hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_bo
     if (!err) err = dmalloc(&cnt, cap);
     if (!err) err = dmalloc(&sums, (cap + per - 1) / per);
     if (!err) err = dmalloc(&total, 1);
+    const auto grid = [](int m) { return dim3((unsigned)((m + kBlock - 1) / kBlock)); };
+    if (!err && sah) {
+        err = dmalloc(&parent, n);
+        if (!err) err = dmalloc(&leaf_parent, n);
+        if (!err) err = dmalloc(&sflags, n);
+        if (!err) err = dmalloc(&cost, n);
+        if (!err) err = dmalloc(&dec, n);
+        if (!err) err = hipMemsetAsync(parent, 0xFF, sizeof(int) * n, s);  // root: -1
+        if (!err) err = hipMemsetAsync(sflags, 0, sizeof(uint32_t) * n, s);
+        if (!err) {
+            hipLaunchKernelGGL(k_sah_parents, grid(n - 1), dim3(kBlock), 0, s, n, children, parent, leaf_parent);
+            hipLaunchKernelGGL(k_sah_dp, grid(n), dim3(kBlock), 0, s, n, parent, leaf_parent, children, ranges,
+                               node_boxes, sorted_vals, prim_boxes, leaf_size, sflags, cost, dec);
+        }
+    }
     int base = 0, items = 1;
     uint32_t levels = 0;  // breadth first: one iteration per BVH4 level
     if (level_start) level_start->clear();
     if (!err) err = hipMemsetAsync(items_a, 0, sizeof(int), s);  // binary root 0
-    const auto grid = [](int m) { return dim3((unsigned)((m + kBlock - 1) / kBlock)); };
     while (!err && items > 0) {
         if (level_start) level_start->push_back((uint32_t)base);
-        hipLaunchKernelGGL(k_collapse_pick, grid(items), dim3(kBlock), 0, s, items, items_a, children, ranges,
-                           node_boxes, leaf_size, clist, cnt);
+        if (sah)
+            hipLaunchKernelGGL(k_collapse_pick_sah, grid(items), dim3(kBlock), 0, s, items, items_a, children, ranges,
+                               dec, leaf_size, clist, cnt);
+        else
+            hipLaunchKernelGGL(k_collapse_pick, grid(items), dim3(kBlock), 0, s, items, items_a, children, ranges,
+                               node_boxes, leaf_size, clist, cnt);
         const int nb = (items + per - 1) / per;
         hipLaunchKernelGGL(k_scan64_blocks, dim3(nb), dim3(kScanBlock), 0, s, cnt, items, sums);
         hipLaunchKernelGGL(k_scan64_sums, dim3(1), dim3(kScanBlock), 0, s, sums, nb, total);
@@ -939,7 +1092,7 @@ hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_bo
     *num_nodes4 = (uint32_t)base;
     *depth4 = levels;
     if (level_start) level_start->push_back((uint32_t)base);
-    void *bufs[] = {items_a, items_b, clist, cnt, sums, total};
+    void *bufs[] = {items_a, items_b, clist, cnt, sums, total, parent, leaf_parent, sflags, cost, dec};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     return err;
@@ -1234,11 +1387,13 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
                                         &out.num_nodes8, &out.depth8, s);
                 out.num_nodes4 = 0;
             } else if (!err && !(collapse && std::strcmp(collapse, "parity") == 0)) {
-                // 4-wide quantized tree, greedy surface-area collapse
+                // 4-wide quantized tree: SAH-optimal slot distribution (PUPIL_BVH4_COLLAPSE=greedy:
+                // greedy surface-area opening)
                 err = dmalloc(&out.nodes4, (size_t)(n - 1));
                 if (!err)
                     err = collapse_bvh4(n, vi, boxes, children, ranges, node_boxes, leaf_size, out.nodes4,
-                                        &out.num_nodes4, &out.depth4, &out.level_start, s);
+                                        &out.num_nodes4, &out.depth4, &out.level_start, s,
+                                        !(collapse && std::strcmp(collapse, "greedy") == 0));
                 const char *order = std::getenv("PUPIL_NODE_ORDER");
                 if (!err && order && out.num_nodes4 > 1) {
                     err = relabel_nodes4(out.nodes4, out.num_nodes4, order, s);
