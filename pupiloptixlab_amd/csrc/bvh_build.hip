@@ -614,8 +614,10 @@ __global__ void k_emit4(int n, const uint32_t *sorted_vals, const Aabb *prim_box
 // it has four children (the wide-BVH collapse of Wald et al. 2008 / Ylitie et
 // al. 2017).  Children that remain internal become the next level's 4-wide
 // nodes, numbered breadth-first after a scan of their counts.
-__device__ __forceinline__ bool opens(int c, const int2 *ranges, uint32_t leaf_size) {
+constexpr uint32_t kSahLeaf = 1u << 12;  // k_sah_dp decision: the subtree is one leaf
+__device__ __forceinline__ bool opens(int c, const int2 *ranges, uint32_t leaf_size, const uint32_t *dec = nullptr) {
     if (c < 0) return false;
+    if (dec) return (dec[c] & kSahLeaf) == 0u;
     const int2 r = ranges[c];
     return (uint32_t)(r.y - r.x + 1) > leaf_size;
 }
@@ -657,7 +659,7 @@ __global__ void k_collapse_pick(int items, const int *item_node, const int2 *chi
 __global__ void k_collapse_emit(int items, int base, int next_base, const int *item_node, const int4 *clist,
                                 const unsigned long long *inner_pos, const uint32_t *sorted_vals,
                                 const Aabb *prim_boxes, const int2 *ranges, const Aabb *node_boxes,
-                                uint32_t leaf_size, int *next_items, Bvh4Node *nodes4) {
+                                uint32_t leaf_size, int *next_items, Bvh4Node *nodes4, const uint32_t *dec) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= items) return;
     const int4 cl = clist[t];
@@ -673,7 +675,7 @@ __global__ void k_collapse_emit(int items, int base, int next_base, const int *i
         if (c < 0) {
             link[nk] = make_leaf((uint32_t)~c, 1u);
             b = prim_boxes[sorted_vals[~c]];
-        } else if (!opens(c, ranges, leaf_size)) {
+        } else if (!opens(c, ranges, leaf_size, dec)) {
             const int2 r = ranges[c];
             link[nk] = make_leaf((uint32_t)r.x, (uint32_t)(r.y - r.x + 1));
             b = node_boxes[c];
@@ -742,7 +744,7 @@ __device__ __forceinline__ float4 sah_cost(int c, const float4 *cost, const uint
 // one thread per primitive walks up; the second child to finish computes its parent
 __global__ void k_sah_dp(int n, const int *parent, const int *leaf_parent, const int2 *children, const int2 *ranges,
                          const Aabb *node_boxes, const uint32_t *sorted_vals, const Aabb *prim_boxes,
-                         uint32_t leaf_size, uint32_t *flags, float4 *cost, uint32_t *dec) {
+                         uint32_t leaf_size, uint32_t sah_leaf, uint32_t *flags, float4 *cost, uint32_t *dec) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     int b = leaf_parent[i];
@@ -772,9 +774,10 @@ __global__ void k_sah_dp(int n, const int *parent, const int *leaf_parent, const
         const int2 r = ranges[b];
         const float a = half_area(node_boxes[b]);
         float c4[4];
-        if ((uint32_t)(r.y - r.x + 1) <= leaf_size) {  // a leaf wherever it goes
-            c4[0] = c4[1] = c4[2] = c4[3] = a * (float)(r.y - r.x + 1);
-            code |= 7u << 8;
+        const uint32_t cnt = (uint32_t)(r.y - r.x + 1);
+        if (cnt <= leaf_size || (cnt <= sah_leaf && a * (float)cnt <= a + d[4])) {  // one leaf wherever it goes
+            c4[0] = c4[1] = c4[2] = c4[3] = a * (float)cnt;
+            code |= 7u << 8 | kSahLeaf;
         } else {
             c4[0] = a + d[4];
             for (int s = 2; s <= 4; s++) {
@@ -810,7 +813,7 @@ __global__ void k_collapse_pick_sah(int items, const int *item_node, const int2 
     while (nw > 0) {
         const int x = wc[--nw];
         int s = wi[nw];
-        if (!opens(x, ranges, leaf_size) || s <= 1) {
+        if (!opens(x, ranges, leaf_size, dec) || s <= 1) {
             c[nk++] = x;
             continue;
         }
@@ -826,7 +829,7 @@ __global__ void k_collapse_pick_sah(int items, const int *item_node, const int2 
         wc[nw] = g.y, wi[nw++] = s - k;
     }
     unsigned long long inner = 0;
-    for (int k = 0; k < nk; k++) inner += opens(c[k], ranges, leaf_size) ? 1ull : 0ull;
+    for (int k = 0; k < nk; k++) inner += opens(c[k], ranges, leaf_size, dec) ? 1ull : 0ull;
     for (int k = nk; k < 4; k++) c[k] = kEmptyLink;
     clist[t] = make_int4(c[0], c[1], c[2], c[3]);
     inner_count[t] = inner;
@@ -1058,8 +1061,11 @@ hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_bo
         if (!err) err = hipMemsetAsync(sflags, 0, sizeof(uint32_t) * n, s);
         if (!err) {
             hipLaunchKernelGGL(k_sah_parents, grid(n - 1), dim3(kBlock), 0, s, n, children, parent, leaf_parent);
+            uint32_t sah_leaf = leaf_size;  // PUPIL_SAH_LEAF: larger leaves where the SAH prefers them (<= 8)
+            if (const char *e = std::getenv("PUPIL_SAH_LEAF"))
+                sah_leaf = (uint32_t)std::min(8, std::max((int)leaf_size, std::atoi(e)));
             hipLaunchKernelGGL(k_sah_dp, grid(n), dim3(kBlock), 0, s, n, parent, leaf_parent, children, ranges,
-                               node_boxes, sorted_vals, prim_boxes, leaf_size, sflags, cost, dec);
+                               node_boxes, sorted_vals, prim_boxes, leaf_size, sah_leaf, sflags, cost, dec);
         }
     }
     int base = 0, items = 1;
@@ -1079,7 +1085,8 @@ hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_bo
         hipLaunchKernelGGL(k_scan64_sums, dim3(1), dim3(kScanBlock), 0, s, sums, nb, total);
         hipLaunchKernelGGL(k_scan64_add, grid(items), dim3(kBlock), 0, s, cnt, items, sums);
         hipLaunchKernelGGL(k_collapse_emit, grid(items), dim3(kBlock), 0, s, items, base, base + items, items_a, clist,
-                           cnt, sorted_vals, prim_boxes, ranges, node_boxes, leaf_size, items_b, nodes4);
+                           cnt, sorted_vals, prim_boxes, ranges, node_boxes, leaf_size, items_b, nodes4,
+                           sah ? dec : nullptr);
         unsigned long long tot = 0;
         (void)hipMemcpyAsync(&tot, total, sizeof(tot), hipMemcpyDeviceToHost, s);
         err = hipStreamSynchronize(s);
