@@ -129,8 +129,10 @@ def main():
     handles = []
 
     def frame():
-        pt.mark_dirty()  # each step is a fresh 8-spp frame from seed 0
-        pt.render(args.spp, stream=stream)
+        # each step renders the next spp samples of a progressive render (seeds advance
+        # by spp, accumulating), as consecutive batches of PTPass::OnRun do; the hint
+        # lets the engine trace the next step's camera rays in this step's last launch
+        pt.render(args.spp, stream=stream, continues=True)
         if gather is not None:  # overlapped with the next frame on a side stream (dist.FrameGather)
             handles.append(gather.gather_async(pt.buffers.get(FINAL_RESULT), stream))
 
@@ -140,17 +142,20 @@ def main():
     torch.cuda.synchronize(dev)
     st_bytes = pt.stats()
 
+    pt.mark_dirty()  # the progressive render starts at seed 0
     for _ in range(args.warmup):
         frame()
     torch.cuda.synchronize(dev)
+    seed_t0 = pt.random_seed  # the timed steps render seeds seed_t0 + k * spp
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    # Frames are enqueued back to back (no host sync inside the timed region);
-    # every step renders the identical frame (seed reset by mark_dirty), so its
-    # ray count is the instrumented frame's, checked against the last frame.
+    # Frames are enqueued back to back (no host sync inside the timed region).  Each
+    # step traces exactly one frame of rays: its camera rays were traced in the previous
+    # step's last launch, and the last step traces those of the step after it; the rays
+    # of the timed frames are counted exactly afterwards by re-rendering them.
     for _ in range(args.steps):
         frame()
     torch.cuda.synchronize(dev)
@@ -158,18 +163,23 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    # exact ray count of the timed frames: each re-rendered (untimed) at its seed
+    rays_local = 0
+    for k in range(args.steps):
+        pt.dirty = False
+        pt.random_seed, pt.sample_cnt = seed_t0 + k * args.spp, 0
+        pt.render(args.spp, collect_stats=1, stream=stream)
+        torch.cuda.synchronize(dev)
+        c = pt.stats()
+        rays_local += c["primary_rays"] + c["extension_rays"] + c["shadow_rays"]
     # one more frame, untimed, with HIP events around every stage launch (the timed
     # frames record none: each event adds ~6 us of stream gap) for the stage times
-    frame_timed = pt.stats()
     pt.mark_dirty()
     pt.render(args.spp, collect_stats=2, stream=stream)
     torch.cuda.synchronize(dev)
     st = pt.stats()
-    assert (st["primary_rays"], st["extension_rays"], st["shadow_rays"]) == \
-        (frame_timed["primary_rays"], frame_timed["extension_rays"], frame_timed["shadow_rays"])
     rays_frame = st["primary_rays"] + st["extension_rays"] + st["shadow_rays"]
     assert rays_frame == st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"]
-    rays_local = rays_frame * args.steps
     ext_ms, trace_ms, shade_ms = st["extend_ms"], st["trace_ms"], st["shade_ms"]
     trace_launches = st["trace_launches"]
 
@@ -240,7 +250,11 @@ def main():
             "config": {"workload": (f"config{args.config}: {n_prims:,}-primitive "
                                     f"{'instanced field' if args.config == 5 else 'sphere field'} ({tris:,} tris), "
                                     f"{args.width}x{args.height}, {args.spp} spp, max_depth {args.max_depth}"),
-                       "frame": f"{args.spp} x PTPass::OnRun", "parallelism": f"tiles{args.tile}x{world}",
+                       "frame": f"{args.spp} x PTPass::OnRun, progressive (step k renders seeds "
+                                f"{args.spp}k..{args.spp}k+{args.spp - 1} of one accumulating render; each step's camera "
+                                "rays ride in the previous step's last launch, PUPIL_HINT_CONTINUE; rays counted "
+                                "exactly per timed frame)",
+                       "parallelism": f"tiles{args.tile}x{world}",
                        "area_emitters": int(desc.num_area_emitters),
                        "accel": "two_level" if st_bytes["two_level"] else "flat",
                        "emitter_select": os.environ.get("PUPIL_EMITTER_SELECT", "guide"),

@@ -202,11 +202,18 @@ typedef struct pupil_pt_launch {
      * events around every stage launch for pupil_pt_stats' per-stage times (each
      * event costs ~6 us of stream gap, so production frames leave it off) */
     uint32_t collect_stats;
-    uint32_t pad;
+    /* bit 0 (PUPIL_HINT_CONTINUE): the next render continues this one (random_seed +
+     * spp, same camera, tiling and spp), as consecutive PTPass::OnRun calls do
+     * (pt_pass.cpp:55-56); the engine then traces the next render's camera rays in
+     * this render's last launch (render-ahead; single-spp renders do so without the
+     * hint).  Output is unchanged either way; a render that does not continue simply
+     * traces its own camera rays.  (Was a padding word: layout unchanged.) */
+    uint32_t hints;
 } pupil_pt_launch;
 
 #define PUPIL_STATS_COUNTERS 1u
 #define PUPIL_STATS_TIMING 2u
+#define PUPIL_HINT_CONTINUE 1u
 
 typedef struct pupil_pt_counters {
     uint64_t primary_rays;

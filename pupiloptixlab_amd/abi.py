@@ -75,7 +75,7 @@ class Launch(C.Structure):
     _fields_ = [("random_seed", C.c_uint32), ("sample_cnt", C.c_uint32), ("spp", C.c_uint32),
                 ("max_depth", C.c_uint32), ("accumulate", C.c_uint32), ("tile_size", C.c_uint32),
                 ("tile_rank", C.c_uint32), ("tile_world", C.c_uint32), ("collect_stats", C.c_uint32),
-                ("pad", C.c_uint32)]
+                ("hints", C.c_uint32)]
 
 
 class Counters(C.Structure):

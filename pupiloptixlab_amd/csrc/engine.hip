@@ -768,7 +768,8 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     // counter renders keep their own primary launch so the counters stay per render)
     const bool use_ahead = pt->ahead_valid && !stats && launch->random_seed == pt->ahead_seed && launch->spp == pt->ahead_spp &&
                            num_local == pt->ahead_local && std::memcmp(key, pt->ahead_key, sizeof(key)) == 0;
-    const bool make_ahead = pt->ahead_mode != 0 && (pt->ahead_mode == 2 || launch->spp == 1) && !stats &&
+    const bool make_ahead = pt->ahead_mode != 0 &&
+                            (pt->ahead_mode == 2 || launch->spp == 1 || (launch->hints & PUPIL_HINT_CONTINUE)) && !stats &&
                             depth >= 2 && pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill != 0 &&
                             paths < (1ull << 30);
     pt->ahead_valid = false;

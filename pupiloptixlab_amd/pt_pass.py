@@ -206,9 +206,12 @@ class PTPass(Pass):
         f.compact = 1 if self.tile[2] > 1 else 0
         return f
 
-    def render(self, spp: int = 1, collect_stats: int = 0, stream=None):
+    def render(self, spp: int = 1, collect_stats: int = 0, stream=None, continues: bool = False):
         """spp consecutive OnRun frames in one wavefront batch (asynchronous).
-        collect_stats: bit 0 counters (node visits, ...), bit 1 per-stage HIP events."""
+        collect_stats: bit 0 counters (node visits, ...), bit 1 per-stage HIP events.
+        continues: the next render() continues this one (progressive rendering), so the
+        engine traces its camera rays ahead (PUPIL_HINT_CONTINUE; single-spp renders
+        always do)."""
         if self.dirty:  # pt_pass.cpp:40-49: camera re-uploaded, accumulation restarted
             if self._world is not None:
                 d = self._world.desc()
@@ -224,6 +227,7 @@ class PTPass(Pass):
         la.accumulate = int(self._accumulate)
         la.tile_size, la.tile_rank, la.tile_world = self.tile
         la.collect_stats = int(collect_stats)
+        la.hints = 1 if continues else 0  # PUPIL_HINT_CONTINUE
         s = stream if stream is not None else self._torch.cuda.current_stream(self.device_index)
         f = self._frame()
         check(self._lib.pupil_pt_render(self._pt, C.byref(f), C.byref(la), C.c_void_p(s.cuda_stream)))

@@ -505,7 +505,7 @@ def test_camera_change_uploads_new_sensor():
     assert np.array_equal(moved.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("case", ["flat", "two_level", "bins", "batched"])
+@pytest.mark.parametrize("case", ["flat", "two_level", "bins", "batched", "hint"])
 def test_render_ahead_onrun_sequence(case, monkeypatch):
     """Render-ahead (engine.hip, PUPIL_AHEAD): the last mixed launch of an OnRun traces
     the camera rays of the next OnRun.  A sequence of OnRuns on one engine must equal
@@ -529,12 +529,12 @@ def test_render_ahead_onrun_sequence(case, monkeypatch):
         w = scenes.sphere_field(8, 48, 32, 4, seed=5, merge=False)
     else:
         w = _cornell(48)
-    spp = 2 if case == "batched" else 1
+    spp = 2 if case in ("batched", "hint") else 1  # hint: PUPIL_HINT_CONTINUE on batched renders
     pt = PTPass(device=0)
     pt.set_scene(w)
 
     def step(k_frames, o, seed0=0, depth=0):
-        pt.render(spp)
+        pt.render(spp, continues=case == "hint")
         torch.cuda.synchronize()
         got = pt.buffers.get("pt accum buffer").cpu().numpy()
         ref = o.render(spp=k_frames * spp, random_seed=seed0, max_depth=depth)["accum"]
@@ -543,7 +543,7 @@ def test_render_ahead_onrun_sequence(case, monkeypatch):
     o = oracle.OracleScene(w.desc())
     for k in range(1, 4):
         step(k, o)
-    if case in ("flat", "batched"):  # the camera moves: accumulation restarts on the new view
+    if case in ("flat", "batched", "hint"):  # the camera moves: accumulation restarts on the new view
         w.set_sensor(40.0, W.look_at_mitsuba((0.3, 1.2, 3.5), (0.0, 0.9, 0.0), (0.0, 1.0, 0.0)), fov_axis="x")
         pt.events.dispatch(Events.CAMERA_CHANGE)
         o = oracle.OracleScene(w.desc())

@@ -21,6 +21,10 @@ def main():
     ap.add_argument("--frames", type=int, default=3)
     ap.add_argument("--spheres", type=int, default=500)
     ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--progressive", type=int, default=0,
+                    help="1: every frame continues the previous one (seeds 8k..8k+7, accumulating) with "
+                         "PUPIL_HINT_CONTINUE, so each frame's camera rays ride in the previous frame's last "
+                         "launch (render-ahead); 0: every frame re-renders seed 0 like bench.py")
     args = ap.parse_args()
     import torch
 
@@ -38,14 +42,15 @@ def main():
         for r in range(n):
             pt.set_tiling(args.tile, r, n)
             pt.mark_dirty()
-            pt.render(8, stream=s)
+            pt.render(8, stream=s, continues=bool(args.progressive))
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             host = 0.0
             for _ in range(args.frames):
-                pt.mark_dirty()
+                if not args.progressive:
+                    pt.mark_dirty()
                 h0 = time.perf_counter()
-                pt.render(8, stream=s)
+                pt.render(8, stream=s, continues=bool(args.progressive))
                 host += time.perf_counter() - h0
             torch.cuda.synchronize()
             per_rank.append((time.perf_counter() - t0) / args.frames * 1e3)
