@@ -9,6 +9,6 @@ bash tools/gpu_round.sh || exit $?
 cd $R
 PROFILE=1 bash tools/gpu_dropin.sh || exit $?
 cd $R
-timeout -k 10 300 python tools/shard_probe.py > gpurun_out/shard_probe.txt 2>&1
+timeout -k 10 300 python tools/shard_probe.py > gpurun_out/shard_probe.txt 2>&1 && timeout -k 10 300 python tools/shard_probe.py --progressive 1 > gpurun_out/shard_probe_prog.txt 2>&1
 rc=$?; echo "shard probe rc=$rc"; tail -n 1 gpurun_out/shard_probe.txt | cut -c1-200
 exit $rc
