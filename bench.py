@@ -163,12 +163,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    # exact ray count of the timed frames: each re-rendered (untimed) at its seed
+    # exact ray count of the timed frames: each re-rendered (untimed) at its seed; every
+    # render logs its per-bounce ray counts (the flags partition), no counter kernels needed
     rays_local = 0
     for k in range(args.steps):
         pt.dirty = False
         pt.random_seed, pt.sample_cnt = seed_t0 + k * args.spp, 0
-        pt.render(args.spp, collect_stats=1, stream=stream)
+        pt.render(args.spp, stream=stream)
         torch.cuda.synchronize(dev)
         c = pt.stats()
         rays_local += c["primary_rays"] + c["extension_rays"] + c["shadow_rays"]
