@@ -163,6 +163,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    # the last timed frame as rank 0 assembles it (--dump / --save)
+    last_frame = None
+    if rank == 0 and (args.dump or args.save):
+        last_frame = handles[-1].synchronize() if gather is not None else pt.buffers.get(FINAL_RESULT).clone()
     # exact ray count of the timed frames: each re-rendered (untimed) at its seed; every
     # render logs its per-bounce ray counts (the flags partition), no counter kernels needed
     rays_local = 0
@@ -227,12 +231,11 @@ def main():
 
     if rank == 0:
         if args.dump:
-            full = handles[-1].synchronize() if gather is not None else pt.buffers.get(FINAL_RESULT)
-            np.save(args.dump, full.cpu().numpy())
+            np.save(args.dump, last_frame.cpu().numpy())
         if args.save:
             from tools import imgio
 
-            img = (handles[-1].synchronize() if gather is not None else pt.buffers.get(FINAL_RESULT)).cpu().numpy()
+            img = last_frame.cpu().numpy()
             imgio.save_render(args.save, img.reshape(args.height, args.width, 4))
         out = {
             "metric": "Mrays/sec + ms/frame, 1M-tri scene @1920x1080 8spp; 1/2/4/8-GPU scaling",

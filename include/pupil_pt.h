@@ -266,6 +266,8 @@ int pupil_pt_set_camera(pupil_pt *pt, const float sample_to_camera[16], const fl
 int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_world[12], const float to_object[12]);
 /* replaces the area-emitter table, selection CDF and env emitter (after an emissive instance moved) */
 int pupil_pt_update_emitters(pupil_pt *pt, const pupil_scene_desc *scene);
+/* Asynchronous on hip_stream (a hipStream_t; NULL = the default null stream): the
+ * output buffers are complete once work later enqueued on that stream runs. */
 int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_launch *launch, void *hip_stream);
 int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out);
 int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank,

@@ -106,7 +106,8 @@ struct pupil_pt {
     bool ahead_valid = false;
     uint32_t ahead_seed = 0, ahead_spp = 0, ahead_local = 0, ahead_half = 0;
     uint32_t ahead_key[5] = {0, 0, 0, 0, 0};
-    hipStream_t last_stream = nullptr;
+    hipStream_t last_stream = nullptr;  // of the last render (NULL = the default stream)
+    bool rendered = false;
     double build_ms = 0.0;
     // path state / queues (grown on demand)
     size_t cap = 0;
@@ -736,7 +737,11 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     const uint32_t ts = launch->tile_size ? launch->tile_size : 32u;
     if (launch->tile_rank >= world) return fail(PUPIL_ERR_INVALID, "tile_rank >= tile_world");
     HIP_TRY(hipSetDevice(pt->device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : pt->own_stream;
+    // NULL is HIP's default (null) stream, as everywhere in HIP: a caller that renders on
+    // it and then reads the output on it (torch's default stream, for one) must see the
+    // frame.  (Until r02 NULL selected the engine's own non-blocking stream, so e.g. a
+    // gather issued on torch's default stream could read a frame still being rendered.)
+    hipStream_t s = (hipStream_t)hip_stream;
 
     // local pixel map (cached per tiling)
     const uint32_t key[5] = {pt->width, pt->height, ts, launch->tile_rank, world};
@@ -773,7 +778,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
                             depth >= 2 && pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill != 0 &&
                             paths < (1ull << 30);
     pt->ahead_valid = false;
-    if (pt->last_stream && s != pt->last_stream) HIP_TRY(hipStreamWaitEvent(s, pt->ev_end, 0));
+    if (pt->rendered && s != pt->last_stream) HIP_TRY(hipStreamWaitEvent(s, pt->ev_end, 0));
     const size_t cap_before = pt->cap;
     int rc = ensure_state(pt, paths * (use_ahead || make_ahead ? 2 : 1));
     if (rc) return rc;
@@ -920,6 +925,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     pt->last_bounces = bounces < 129 ? bounces : 129;  // rays are logged for bounces 0..127
     pt->last_stats = stats;
     pt->last_stream = s;
+    pt->rendered = true;
     return PUPIL_OK;
 }
 

@@ -566,6 +566,29 @@ def test_render_ahead_onrun_sequence(case, monkeypatch):
     pt.close_engine()
 
 
+def test_render_orders_with_torch_default_stream():
+    """A render enqueued on torch's default stream (handle NULL) runs on that stream: a
+    read on the same stream right after it, with no device synchronisation, sees the
+    finished frame (r02: NULL used to select the engine's own non-blocking stream, and
+    the multi-rank gather could copy a frame still being rendered)."""
+    import torch
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    w = _cornell(96)
+    pt = PTPass(device=0)
+    pt.set_scene(w)
+    assert torch.cuda.current_stream().cuda_stream == 0
+    frames = []
+    for _ in range(3):
+        pt.render(4, continues=True)
+        frames.append(pt.buffers.get("pt accum buffer").cpu().numpy())  # ordered on the same stream
+    pt.close_engine()
+    o = oracle.OracleScene(w.desc())
+    for k, got in enumerate(frames):
+        ref = o.render(spp=4 * (k + 1))["accum"]
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), f"frame {k}"
+
+
 @pytest.mark.parametrize("accel", ["flat", "two_level"])
 def test_skewed_scene_stays_within_stack_capacity(accel, monkeypatch):
     """A geometric chain of triangles (size and spacing x1.15 per triangle) makes the
