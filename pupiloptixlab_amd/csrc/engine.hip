@@ -595,9 +595,11 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pt->device);
     sc.num_cus = (uint32_t)std::max(1, cus);
-    sc.trace_refill = 24;  // persistent BVH4 kernels; 0 selects the one-ray-per-lane kernels (A/B)
+    // persistent BVH4 kernels: refill once 16 lanes are idle (r02 re-tune on the SAH tree:
+    // 16 / 12 beat 20 / 24 by ~0.7 % at N = 1 and the 8-way shard; 0 = one-ray-per-lane A/B)
+    sc.trace_refill = 16;
     if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
-    if ((pt->two_level || sc.bvh_width == 8) && sc.trace_refill == 0) sc.trace_refill = 24;  // persistent kernels only
+    if ((pt->two_level || sc.bvh_width == 8) && sc.trace_refill == 0) sc.trace_refill = 16;  // persistent kernels only
     if (const char *po = std::getenv("PUPIL_PRIMARY_ORDER")) pt->primary_interleave = std::strcmp(po, "path") != 0;
     {  // one material bin in the whole scene: the material partition orders nothing (auto; =bins / =list force)
         uint32_t bins = 0;
