@@ -45,6 +45,8 @@ int main(void) {
   S(pupil_scene_desc) S(pupil_pt_frame) S(pupil_pt_launch) S(pupil_pt_counters)
   O(pupil_texture, rgba) O(pupil_material, tex) O(pupil_instance, emitter_offset) O(pupil_emitter, radiance)
   O(pupil_emitter, scale) O(pupil_scene_desc, shapes) O(pupil_scene_desc, env) O(pupil_pt_counters, trace_launches)
+  O(pupil_pt_launch, collect_stats) O(pupil_pt_launch, hints)
+  printf("PUPIL_HINT_CONTINUE %u\n", PUPIL_HINT_CONTINUE);
   return 0;
 }
 """
@@ -64,6 +66,7 @@ def test_struct_layouts_match_c(tmp_path):
           "pupil_pt_frame": abi.Frame, "pupil_pt_launch": abi.Launch, "pupil_pt_counters": abi.Counters}
     for cname, cls in py.items():
         assert int(got[cname]) == C.sizeof(cls), cname
+    assert int(got["PUPIL_HINT_CONTINUE"]) == 1  # what PTPass.render(continues=True) sets
     for key, val in got.items():
         if "." in key:
             cname, field = key.split(".")
