@@ -35,7 +35,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=4,
+                    help="untimed steps; max_depth of them fill the frame pipeline (one traversal launch per step)")
     ap.add_argument("--config", type=int, default=4, choices=(3, 4, 5),
                     help="BASELINE.json configs[k-1]: 3 = 250k-tri field, 4 = 1M-tri field (headline), "
                          "5 = 40 x 250k-tri instanced rough dielectric/plastic field, 3840x2160 16 spp D6")
@@ -130,32 +131,34 @@ def main():
 
     def frame():
         # each step renders the next spp samples of a progressive render (seeds advance
-        # by spp, accumulating), as consecutive batches of PTPass::OnRun do; the hint
-        # lets the engine trace the next step's camera rays in this step's last launch
-        pt.render(args.spp, stream=stream, continues=True)
+        # by spp, accumulating), as consecutive batches of PTPass::OnRun do; the hint lets
+        # the engine pipeline frames (engine.hip render_pipelined: the step's one traversal
+        # launch also advances the frames of the next steps).  collect_stats=4: HIP events
+        # around the traversal launches only, summed over the timed steps
+        pt.render(args.spp, stream=stream, continues=True, collect_stats=4)
         if gather is not None:  # overlapped with the next frame on a side stream (dist.FrameGather)
             handles.append(gather.gather_async(pt.buffers.get(FINAL_RESULT), stream))
 
-    # one instrumented frame for the traversal byte counts (untimed)
+    # one instrumented frame (untimed, rendered on its own) for the traversal counters:
+    # node visits / primitive tests per ray, the algorithmic bytes of SURVEY.md §8(d)
     pt.mark_dirty()
     pt.render(args.spp, collect_stats=1, stream=stream)
     torch.cuda.synchronize(dev)
     st_bytes = pt.stats()
+    rays_counter_frame = st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"]
 
     pt.mark_dirty()  # the progressive render starts at seed 0
     for _ in range(args.warmup):
         frame()
     torch.cuda.synchronize(dev)
-    seed_t0 = pt.random_seed  # the timed steps render seeds seed_t0 + k * spp
+    c0 = pt.stats()  # also restarts the traversal-event sum
+    seed_t0 = pt.random_seed
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    # Frames are enqueued back to back (no host sync inside the timed region).  Each
-    # step traces exactly one frame of rays: its camera rays were traced in the previous
-    # step's last launch, and the last step traces those of the step after it; the rays
-    # of the timed frames are counted exactly afterwards by re-rendering them.
+    # Frames are enqueued back to back (no host sync inside the timed region).
     for _ in range(args.steps):
         frame()
     torch.cuda.synchronize(dev)
@@ -163,32 +166,31 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    # the last timed frame as rank 0 assembles it (--dump / --save)
+    # exact work of the timed steps: the rays their launches traced (device running totals
+    # of the flags partitions + the camera rays), whichever frame they belong to
+    c1 = pt.stats()
+    rays_local = c1["rays_traced_total"] - c0["rays_traced_total"]
+    timed = {"trace_ms": c1["trace_ms"], "launches": c1["trace_launches"], "rays": rays_local,
+             "frames_in_flight": c1["frames_in_flight"], "pipeline_slots": c1["pipeline_slots"]}
+    # the last timed frame (seeds 0 .. seed_t0 + steps*spp - 1 accumulated), checked below
+    last_accum = pt.buffers.get("pt accum buffer").clone() if rank == 0 and world == 1 else None
     last_frame = None
     if rank == 0 and (args.dump or args.save):
         last_frame = handles[-1].synchronize() if gather is not None else pt.buffers.get(FINAL_RESULT).clone()
-    # exact ray count of the timed frames: each re-rendered (untimed) at its seed; every
-    # render logs its per-bounce ray counts (the flags partition), no counter kernels needed
-    rays_local = 0
-    for k in range(args.steps):
-        pt.dirty = False
-        pt.random_seed, pt.sample_cnt = seed_t0 + k * args.spp, 0
-        pt.render(args.spp, stream=stream)
-        torch.cuda.synchronize(dev)
-        c = pt.stats()
-        rays_local += c["primary_rays"] + c["extension_rays"] + c["shadow_rays"]
-    # one more frame, untimed, with HIP events around every stage launch (the timed
-    # frames record none: each event adds ~6 us of stream gap) for the stage times
+    # one more frame, untimed, rendered on its own with HIP events around every stage
+    # launch (stage times; each event adds ~6 us of stream gap)
     pt.mark_dirty()
     pt.render(args.spp, collect_stats=2, stream=stream)
     torch.cuda.synchronize(dev)
     st = pt.stats()
     rays_frame = st["primary_rays"] + st["extension_rays"] + st["shadow_rays"]
-    assert rays_frame == st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"]
+    assert rays_frame == rays_counter_frame
     ext_ms, trace_ms, shade_ms = st["extend_ms"], st["trace_ms"], st["shade_ms"]
-    trace_launches = st["trace_launches"]
+    # rays traced by the plain (non-counter) traversal kernels over this process: the
+    # denominator of the per-ray PMC figures (tools/pmc_summary.py --json)
+    rays_plain_process = st["rays_traced_total"] - rays_counter_frame
 
-    t = torch.tensor([elapsed, float(rays_local), trace_ms], dtype=torch.float64,
+    t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64,
                      device=dev if backend == "nccl" else "cpu")
     if world > 1:
         t_max = t.clone()
@@ -201,14 +203,15 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     mrays = rays_total / elapsed / 1e6
-    rays_frame_local = st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"]
-    # roofline of the dominant kernel, the persistent BVH4 traversal k_trace4 (per
-    # frame: the primary extend launch, then one launch per bounce over the
-    # concatenated extension + shadow lists).  Three ceilings are evaluated and the
-    # binding (highest) one is reported: dependent node gathers (live node-visit
-    # rate / the gather ceiling measured on this box by build/ubench_gather), VALU
-    # issue and HBM bytes (both from the committed PMC passes of this config).
-    roof = roofline(args, st_bytes, trace_ms, trace_launches) if rank == 0 else None
+    rays_frame_local = rays_counter_frame
+    # roofline of the dominant kernel, the persistent BVH4 traversal k_trace4 (pipelined:
+    # one launch per step over the shadow + extension rays of every frame in flight and
+    # the camera rays of the newest).  Three ceilings are evaluated and the binding
+    # (highest) one is reported: dependent node gathers (live node-visit rate / the
+    # gather ceiling measured on this box by build/ubench_gather), VALU issue and HBM
+    # bytes (per-ray figures of the committed PMC passes of this config, times this
+    # rank's rays per launch).  Launch time: HIP events around the timed steps' launches.
+    roof = roofline(args, st_bytes, timed) if rank == 0 else None
     update = None
     if args.config == 5 and rank == 0:  # RenderInstanceUpdate cost: move instance 0, re-sync the accel
         from pupiloptixlab_amd import world as W
@@ -223,11 +226,13 @@ def main():
 
     dropin = None
     if rank == 0 and world == 1 and args.dropin and args.config in (3, 4) and args.emissive_groups == 0:
-        dropin = dropin_cadence(args, ms_per_step, mrays)
+        dropin = dropin_cadence(args, ms_per_step, last_accum)
 
     cpu = None
+    timed_check = None
     if rank == 0 and world == 1 and args.cpu_baseline and args.emissive_groups == 0:
         cpu = cpu_baseline(desc, args, pt)
+        timed_check = timed_frame_check(desc, args, last_accum, seed_t0 + args.steps * args.spp)
 
     if rank == 0:
         if args.dump:
@@ -255,14 +260,20 @@ def main():
                                     f"{'instanced field' if args.config == 5 else 'sphere field'} ({tris:,} tris), "
                                     f"{args.width}x{args.height}, {args.spp} spp, max_depth {args.max_depth}"),
                        "frame": f"{args.spp} x PTPass::OnRun, progressive (step k renders seeds "
-                                f"{args.spp}k..{args.spp}k+{args.spp - 1} of one accumulating render; each step's camera "
-                                "rays ride in the previous step's last launch, PUPIL_HINT_CONTINUE; rays counted "
-                                "exactly per timed frame)",
+                                f"{args.spp}k..{args.spp}k+{args.spp - 1} of one accumulating render, "
+                                "PUPIL_HINT_CONTINUE: frames pipelined, each step's one traversal launch advances "
+                                "every frame in flight by a bounce and the step's own frame is complete when it "
+                                "returns; value counts exactly the rays the timed steps' launches traced)",
+                       "pipeline": {"slots": int(timed["pipeline_slots"]),
+                                    "frames_in_flight_after": int(timed["frames_in_flight"]),
+                                    "traversal_launches_timed": int(timed["launches"])},
+                       "rays_traced_plain_process": int(rays_plain_process),
                        "parallelism": f"tiles{args.tile}x{world}",
                        "area_emitters": int(desc.num_area_emitters),
                        "accel": "two_level" if st_bytes["two_level"] else "flat",
                        "emitter_select": os.environ.get("PUPIL_EMITTER_SELECT", "guide"),
-                       "rays_per_frame": rays_total / args.steps,
+                       "rays_per_step": rays_total / args.steps,
+                       "rays_per_frame_rank0": int(rays_frame_local),
                        # shadow rays the reference would trace (one per loop iteration past RR,
                        # main.cu:119-123); the engine and the oracle trace one only when the
                        # contribution is non-zero (radiance-equivalent: Eval draws no random
@@ -291,16 +302,20 @@ def main():
             "instance_update_ms": update,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "timed_frame_bit_exact": timed_check,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def dropin_cadence(args, batched_ms, batched_mrays):
+def dropin_cadence(args, batched_ms, last_accum):
     """The reference's cadence through the C++ drop-in: examples/path_tracer (System +
-    PTPass, pt_pass.cpp:39-57: one 1-spp launch per OnRun, then a stream sync) on
-    this scene exported as XML + OBJ (scenes.XmlWorld; loads bit-identically)."""
+    PTPass, pt_pass.cpp:39-57: one 1-spp render per OnRun, then a stream sync) on this
+    scene exported as XML + OBJ (scenes.XmlWorld; loads bit-identically), as a
+    progressive sequence of the same length as the bench's (warmup + steps frames of
+    spp OnRuns).  Its final accumulation buffer must equal the bench's last timed frame
+    (same seeds) bit for bit."""
     import subprocess
     import tempfile
 
@@ -313,16 +328,22 @@ def dropin_cadence(args, batched_ms, batched_mrays):
         xw = scenes.XmlWorld()
         scenes.sphere_field(args.spheres, args.width, args.height, args.max_depth, seed=1, world=xw)
         path = xw.save(os.path.join(tmp, f"config{args.config}.xml"))
-        env = dict(os.environ, PUPIL_BENCH=f"2,{max(3, args.steps)},{args.spp}")
+        accum_path = os.path.join(tmp, "accum.f32")
+        env = dict(os.environ, PUPIL_BENCH=f"{args.warmup},{args.steps},{args.spp}", PUPIL_BENCH_ACCUM=accum_path)
         try:
             r = subprocess.run([exe, path], capture_output=True, text=True, timeout=600, env=env)
             rec = json.loads(r.stdout.strip().splitlines()[-1])
+            cpp = np.fromfile(accum_path, np.float32).reshape(-1, 4)
         except (OSError, ValueError, IndexError, subprocess.SubprocessError) as e:
             return {"error": f"{type(e).__name__}: {e}"}
+    if last_accum is not None:
+        gpu = last_accum.cpu().numpy().reshape(-1, 4)
+        same = int(np.all(gpu.view(np.uint32) == cpp.view(np.uint32), axis=1).sum()) if gpu.shape == cpp.shape else 0
+        rec["bit_exact"] = f"{same}/{len(gpu)}"
     rec["vs_batched_ms"] = round(rec["ms_per_frame"] / batched_ms, 3) if batched_ms > 0 else None
     rec["what"] = (f"{args.spp} x C++ PTPass::OnRun (1 spp + hipStreamSynchronize each) per frame, "
-                   "examples/path_tracer on the exported XML; value/ms_per_step above batch the frame's spp "
-                   "in one launch sequence")
+                   f"{args.warmup} + {args.steps} frames of one progressive render, examples/path_tracer on the "
+                   "exported XML; bit_exact: its final accumulation vs the bench's last timed frame (same seeds)")
     return rec
 
 
@@ -333,31 +354,34 @@ def default_config(args):
 
 
 def pmc_record(args):
-    """Per-launch PMC figures of k_trace4 for this config (tools/gpu_pmc.sh ->
-    tools/pmc_summary.py --json, committed as profiles/pmc_config<k>.json): HBM
-    bytes (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md), VALU instructions and GRBM cycles.  None when absent or
-    when this run is not the default configuration the passes were taken on."""
+    """Per-ray PMC figures of the plain k_trace4 launches for this config (tools/gpu_pmc.sh
+    -> tools/pmc_summary.py --json, committed as profiles/pmc_config<k>.json): HBM bytes
+    (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md) and VALU
+    instructions per traced ray, and the GRBM clock.  Per ray, so that they apply to any
+    launch size: pipelined launches, and one rank's tiles at N > 1.  None when absent or
+    when this run is not the scene the passes were taken on."""
     path = os.path.join(HERE, "profiles", f"pmc_config{args.config}.json")
     if not default_config(args) or not os.path.exists(path):
         return None
     try:
         with open(path) as f:
-            return json.load(f)
+            rec = json.load(f)
     except (OSError, ValueError):
         return None
+    return rec if rec.get("traffic_bytes_per_ray") else None
 
 
-def gather_ceiling(bvh_nodes):
+def gather_ceiling(footprint_bytes):
     """Dependent random 64-B gather ceiling of this GPU (G fetches/s), measured now by
-    build/ubench_gather on a table of 2^floor(log2(bvh_nodes)) nodes (no larger
-    than the scene's node array, so the ceiling is not understated)."""
+    build/ubench_gather on a table of the next power of two above the traversal's
+    footprint (BVH nodes + primitive records), so the ceiling is not overstated by a
+    table that caches better than the real arrays."""
     import subprocess
 
     exe = os.path.join(HERE, "build", "ubench_gather")
     if not os.path.exists(exe):
         return None
-    log2 = max(12, int(np.floor(np.log2(max(2, bvh_nodes)))))
+    log2 = max(12, int(np.ceil(np.log2(max(2.0, footprint_bytes / 64.0)))))
     try:
         r = subprocess.run([exe, str(log2), "--json"], capture_output=True, text=True, timeout=120)
         return json.loads(r.stdout.strip().splitlines()[-1])
@@ -365,49 +389,56 @@ def gather_ceiling(bvh_nodes):
         return None
 
 
-def roofline(args, st_bytes, trace_ms, trace_launches):
-    # the counter frame records no stage events; its traversal launches are the timing frame's
-    launches = max(1, trace_launches)
-    ms = trace_ms / launches  # HIP events on the render stream, the extra timing frame
+def roofline(args, st_bytes, timed):
+    """st_bytes: the counter frame's stats (per-ray node visits, primitive tests, bytes);
+    timed: this rank's timed steps -- summed traversal launch time (HIP events on the
+    render stream), launches, rays traced."""
+    launches = max(1, timed["launches"])
+    ms = timed["trace_ms"] / launches
     sec = ms * 1e-3
-    visits = st_bytes["node_visits"] / launches
+    rays_cf = max(1, st_bytes["primary_rays"] + st_bytes["extension_rays"] + st_bytes["shadow_rays"])
+    rays_launch = timed["rays"] / launches
+    per_launch = lambda k: st_bytes[k] / rays_cf * rays_launch  # noqa: E731
+    visits = per_launch("node_visits")
     # lanes of a wave on the same node share one fetch: the distinct fetches per wave step are
     # the gathers the memory system serves, the quantity the random-gather ceiling measures
-    nodes = (st_bytes.get("unique_node_fetches") or st_bytes["node_visits"]) / launches
-    alg_bytes = st_bytes["trace_bytes"] / launches
-    kernel = ("k_trace4 (persistent BVH4 traversal, all launches of a frame: primary extend + "
-              "per-bounce extension+shadow)")
+    nodes = per_launch("unique_node_fetches") if st_bytes.get("unique_node_fetches") else visits
+    alg_bytes = per_launch("trace_bytes")
+    kernel = ("k_trace4 (persistent BVH4 traversal; pipelined frames: one launch per step over the shadow + "
+              "extension rays of every frame in flight and the newest frame's camera rays)")
     cands = {}
-    ceil = gather_ceiling(int(st_bytes["bvh_nodes"]))
+    footprint = 64.0 * st_bytes["bvh_nodes"] + 48.0 * st_bytes["bvh_prims"]
+    ceil = gather_ceiling(footprint)
     if ceil and sec > 0:
         cands["node-gather"] = {"achieved": nodes / sec / 1e9, "peak": ceil["ceiling_gnodes_per_s"],
                                 "unit": "Gnode/s",
-                                "how": "distinct node fetches per wave step, per launch (counter frame) / HIP-event "
-                                       "launch time; peak = build/ubench_gather dependent random 64-B gathers, "
-                                       f"{ceil['table_mb']:.0f} MB table (the BVH's size), best waves/SIMD, measured in "
-                                       "this run",
+                                "how": "distinct node fetches per ray (counter frame) x rays per launch / HIP-event "
+                                       "launch time; peak = build/ubench_gather dependent random 64-B gathers on a "
+                                       f"{ceil['table_mb']:.0f} MB table (>= the BVH nodes + primitive records, "
+                                       f"{footprint / 1e6:.0f} MB), best waves/SIMD, measured in this run",
                                 "node_visits_per_launch": round(visits, 1),
                                 "distinct_fetches_per_launch": round(nodes, 1),
                                 "ceiling_per_waves_per_simd": ceil.get("per_waves_per_simd")}
     pmc = pmc_record(args)
     traffic = None
     if pmc and sec > 0:
-        traffic = pmc["traffic_bytes_per_launch"]
+        traffic = pmc["traffic_bytes_per_ray"] * rays_launch
         cands["hbm"] = {"achieved": traffic / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "how": "PMC 2 x FETCH_SIZE + WRITE_SIZE per launch (profiles/pmc_config%d.json, %s) / "
-                               "HIP-event launch time" % (args.config, pmc.get("round", "?"))}
-        if pmc.get("valu_insts_per_launch") and pmc.get("clock_ghz"):
+                        "how": "PMC (2 x FETCH_SIZE + WRITE_SIZE) per traced ray (profiles/pmc_config%d.json, %s) x "
+                               "rays per launch / HIP-event launch time" % (args.config, pmc.get("round", "?"))}
+        if pmc.get("valu_insts_per_ray") and pmc.get("clock_ghz"):
             simds = 1024  # 256 CUs x 4 SIMD
             # wave64 VALU op = 2 issue cycles on a SIMD-32 (MI355X_MICROARCH.md)
-            need = 2.0 * pmc["valu_insts_per_launch"]
-            have = simds * pmc["clock_ghz"] * 1e9 * sec
-            cands["valu-issue"] = {"achieved": need / sec / 1e9, "peak": simds * pmc["clock_ghz"], "unit": "G SIMD-cycles/s",
-                                   "how": "PMC SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) per launch over 1024 SIMDs at "
-                                          "the GRBM-measured clock"}
+            need = 2.0 * pmc["valu_insts_per_ray"] * rays_launch
+            cands["valu-issue"] = {"achieved": need / sec / 1e9, "peak": simds * pmc["clock_ghz"],
+                                   "unit": "G SIMD-cycles/s",
+                                   "how": "PMC SQ_INSTS_VALU per traced ray x rays per launch x 2 cycles (wave64 on "
+                                          "SIMD-32) over 1024 SIMDs at the GRBM-measured clock"}
     for c in cands.values():
         c["frac"] = round(c["achieved"] / c["peak"], 4)
         c["achieved"] = round(c["achieved"], 2)
-    out = {"kernel": kernel, "ms_per_launch": round(ms, 4), "traffic": round(traffic, 1) if traffic else None,
+    out = {"kernel": kernel, "ms_per_launch": round(ms, 4), "launches": int(launches),
+           "rays_per_launch": round(rays_launch, 1), "traffic": round(traffic, 1) if traffic else None,
            # SURVEY.md §8(d) algorithmic bytes (32 B ray + 16 B hit + 64 B/node + 48 B/primitive): the BVH
            # is cache-resident (L2 + Infinity Cache), so these exceed what HBM delivers; not a fraction of HBM
            "algorithmic": {"bytes_per_launch": round(alg_bytes, 1),
@@ -453,6 +484,28 @@ def native_oracle():
         return out
     except (OSError, subprocess.SubprocessError):
         return None
+
+
+def timed_frame_check(desc, args, last_accum, n_frames):
+    """The last timed frame (a progressive render of seeds 0 .. n_frames - 1, most of it
+    pipelined) against the oracle rendering the same n_frames OnRuns, on every k-th pixel
+    (k = 64 for configs 3/4, 1024 for config 5); bit-exact expected."""
+    if last_accum is None:
+        return None
+    try:
+        import oracle
+    except Exception as e:  # pragma: no cover
+        return {"error": str(e)}
+    stride = 1024 if args.config == 5 else 64
+    npix = args.width * args.height
+    pixels = np.arange(stride // 2, npix, stride, dtype=np.uint32)
+    osc = oracle.OracleScene(desc)
+    r = osc.render(spp=n_frames, max_depth=args.max_depth, pixels=pixels, threads=args.cpu_threads or usable_cpus())
+    osc.close()
+    gpu = last_accum.cpu().numpy().reshape(npix, 4)[pixels]
+    exact = int(np.all(gpu.view(np.uint32) == r["accum"].view(np.uint32), axis=1).sum())
+    return {"pixels": f"every {stride}th pixel from {stride // 2}", "frames": int(n_frames),
+            "bit_exact": f"{exact}/{len(pixels)}"}
 
 
 def cpu_baseline(desc, args, pt):

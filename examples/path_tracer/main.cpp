@@ -17,42 +17,50 @@
 #include "pupil/pt_pass.h"
 
 // PUPIL_BENCH="warmup,frames,spp": the drop-in cadence of the reference
-// (pt_pass.cpp:39-57): a frame is `spp` x System::Run(1), i.e. spp x
-// PTPass::OnRun of 1 spp each with its stream synchronisation; each frame
-// restarts accumulation through a CameraChange event.  One untimed frame
-// counts the rays (pupil_pt_stats after every OnRun); then `warmup` untimed
-// and `frames` timed frames (steady_clock around the whole loop).  Prints one
-// JSON line.
+// (pt_pass.cpp:39-57): a frame is `spp` x System::Run(1), i.e. spp x PTPass::OnRun
+// of 1 spp each with its stream synchronisation, and the frames continue one
+// progressive render (accumulation restarts once, through a CameraChange event, as
+// when the user stops moving the camera).  `warmup` untimed and `frames` timed frames
+// (steady_clock around the loop); the rays are the engine's exact running total over
+// the timed OnRuns.  PUPIL_BENCH_ACCUM=<file>: the final "pt accum buffer" (rank 0,
+// raw float32 RGBA) for a bit-exact comparison with a batched render of the same
+// seeds.  Prints one JSON line.
 static int Bench(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spec) {
     int warmup = 1, frames = 5, spp = 8;
-    if (std::sscanf(spec, "%d,%d,%d", &warmup, &frames, &spp) != 3 || frames < 1 || spp < 1) {
+    if (std::sscanf(spec, "%d,%d,%d", &warmup, &frames, &spp) != 3 || frames < 1 || spp < 1 || warmup < 0) {
         std::fprintf(stderr, "PUPIL_BENCH must be warmup,frames,spp\n");
         return 2;
     }
-    auto frame = [&]() {
-        Pupil::EventDispatcher<Pupil::EWorldEvent::CameraChange>();
-        system.Run((uint32_t)spp);
-    };
     Pupil::EventDispatcher<Pupil::EWorldEvent::CameraChange>();
-    double rays = 0.0;
-    for (int k = 0; k < spp; k++) {
-        system.Run(1);
-        pupil_pt_counters c{};
-        if (!pass.Stats(c)) return 1;
-        rays += (double)(c.primary_rays + c.extension_rays + c.shadow_rays);
-    }
-    for (int k = 0; k < warmup; k++) frame();
+    for (int k = 0; k < warmup; k++) system.Run((uint32_t)spp);
     if (hipDeviceSynchronize() != hipSuccess) return 1;
+    pupil_pt_counters c0{}, c1{};
+    if (!pass.Stats(c0)) return 1;
     const auto t0 = std::chrono::steady_clock::now();
-    for (int k = 0; k < frames; k++) frame();
+    for (int k = 0; k < frames; k++) system.Run((uint32_t)spp);
     if (hipDeviceSynchronize() != hipSuccess) return 1;
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!pass.Stats(c1)) return 1;
+    const double rays = (double)(c1.rays_traced_total - c0.rays_traced_total);
     Pupil::FrameGather *g = system.Gather();
     if (g && g->Info().rank != 0) return 0;
+    if (const char *path = std::getenv("PUPIL_BENCH_ACCUM")) {
+        auto *buf = Pupil::BufferManager::instance()->GetBuffer("pt accum buffer");
+        const size_t n = buf ? (size_t)buf->desc.width * buf->desc.height * 4 : 0;
+        std::vector<float> host(n);
+        if (!buf || hipMemcpy(host.data(), buf->cuda_ptr, n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+            return 1;
+        FILE *f = std::fopen(path, "wb");
+        if (!f || std::fwrite(host.data(), sizeof(float), n, f) != n) {
+            if (f) std::fclose(f);
+            return 1;
+        }
+        std::fclose(f);
+    }
     std::printf("{\"ms_per_frame\": %.4f, \"onrun_ms\": %.4f, \"mrays_per_s_rank0\": %.2f, \"rays_per_frame_rank0\": %.0f, "
-                "\"frames\": %d, \"warmup\": %d, \"spp\": %d, \"ranks\": %d}\n",
-                1e3 * s / frames, 1e3 * s / (frames * spp), rays * frames / s / 1e6, rays, frames, warmup, spp,
-                g ? g->Info().world : 1);
+                "\"frames\": %d, \"warmup\": %d, \"spp\": %d, \"ranks\": %d, \"frames_in_flight\": %llu}\n",
+                1e3 * s / frames, 1e3 * s / (frames * spp), rays / s / 1e6, rays / frames, frames, warmup, spp,
+                g ? g->Info().world : 1, (unsigned long long)c1.frames_in_flight);
     return 0;
 }
 

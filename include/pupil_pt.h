@@ -11,7 +11,8 @@
  *   pupil_pt_set_camera      — CameraHelper::GetCudaMemory upload (framework/world/camera.cpp:72-91)
  *   pupil_pt_update_instance — IASManager::UpdateInstance + IAS::Update
  *                              (framework/world/ias_manager.cpp:116-151,187-211); the engine
- *                              rebuilds its (flattened) BVH over the moved primitives
+ *                              refits its BVH over the moved primitives (topology kept, like
+ *                              IAS::Update; PUPIL_FLAT_UPDATE / PUPIL_TL_UPDATE=rebuild rebuild it)
  *   pupil_pt_update_emitters — EmitterHelper reset on RenderInstanceUpdate (world/world.cpp:45-54)
  *   pupil_pt_render          — PTPass::OnRun: optixLaunch(w,h,1) + sync, repeated spp times
  *                              with random_seed++ / sample_cnt += accumulate
@@ -201,18 +202,25 @@ typedef struct pupil_pt_launch {
      * reference's shadow-ray count (slower kernels); bit 1 (PUPIL_STATS_TIMING): HIP
      * events around every stage launch for pupil_pt_stats' per-stage times (each
      * event costs ~6 us of stream gap, so production frames leave it off) */
+    /* bit 2 (PUPIL_STATS_TRACE_TIMING): events around the traversal launches only (two
+     * per launch); their times are summed over every render since pupil_pt_stats last
+     * read them, so a timed sequence of renders reports its own traversal time */
     uint32_t collect_stats;
-    /* bit 0 (PUPIL_HINT_CONTINUE): the next render continues this one (random_seed +
-     * spp, same camera, tiling and spp), as consecutive PTPass::OnRun calls do
-     * (pt_pass.cpp:55-56); the engine then traces the next render's camera rays in
-     * this render's last launch (render-ahead; single-spp renders do so without the
-     * hint).  Output is unchanged either way; a render that does not continue simply
-     * traces its own camera rays.  (Was a padding word: layout unchanged.) */
+    /* bit 0 (PUPIL_HINT_CONTINUE): the next renders continue this one (random_seed +
+     * spp each, same camera, scene, tiling, spp and max_depth), as consecutive
+     * PTPass::OnRun calls do (pt_pass.cpp:55-56).  The engine then pipelines frames:
+     * this render's launches also start the frames of the renders after it (camera
+     * rays and first bounces, up to max_depth frames in flight), so a continued
+     * sequence costs one traversal launch per render.  The render's own frame is
+     * complete when its work has run, as without the hint; single-spp renders
+     * pipeline without it.  Output is bit-identical either way; a render that does not
+     * continue drops the frames ahead and renders its own.  (Was a padding word.) */
     uint32_t hints;
 } pupil_pt_launch;
 
 #define PUPIL_STATS_COUNTERS 1u
 #define PUPIL_STATS_TIMING 2u
+#define PUPIL_STATS_TRACE_TIMING 4u
 #define PUPIL_HINT_CONTINUE 1u
 
 typedef struct pupil_pt_counters {
@@ -226,7 +234,8 @@ typedef struct pupil_pt_counters {
     uint64_t bvh_prims;
     double build_ms;
     double last_render_ms;   /* device time of the last pupil_pt_render (events) */
-    double trace_ms;         /* device time of the traversal kernels in the last render */
+    double trace_ms;         /* device time of the traversal kernels in the last render (collect_stats
+                              * bit 1), or in every PUPIL_STATS_TRACE_TIMING render since the last read */
     double trace_bytes;      /* algorithmic bytes of the traversal kernels (collect_stats) */
     uint64_t trace_launches;
     /* the dominant kernel (closest-hit extend) on its own: device time, launches,
@@ -252,6 +261,16 @@ typedef struct pupil_pt_counters {
      * lanes of a wave on the same node share one fetch) -- the gather rate the memory
      * system serves, comparable with independent random gathers */
     uint64_t unique_node_fetches;
+    /* ABI 3.  Rays (camera + extension + shadow) traced since the engine was created, by
+     * every render: the exact work of a timed sequence of pipelined renders, whose
+     * launches also trace rays of the frames ahead of them */
+    uint64_t rays_traced_total;
+    /* frames started ahead of the next render (pipelined frames) and the ring size */
+    uint64_t frames_in_flight;
+    uint64_t pipeline_slots;
+    /* two-level structure: TLAS nodes whose children were chosen by the binned SAH (an
+     * entry range too large for the exact split search, accel_two_level.hip) */
+    uint64_t tlas_sah_splits;
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;

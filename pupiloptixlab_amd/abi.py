@@ -87,7 +87,10 @@ class Counters(C.Structure):
                 ("extend_ms", C.c_double), ("extend_launches", C.c_uint64), ("extend_node_visits", C.c_uint64),
                 ("extend_prim_tests", C.c_uint64), ("extend_bytes", C.c_double), ("shade_ms", C.c_double),
                 ("two_level", C.c_uint64), ("shadow_rays_reference", C.c_uint64),
-                ("bvh_depth", C.c_uint64), ("unique_node_fetches", C.c_uint64)]
+                ("bvh_depth", C.c_uint64), ("unique_node_fetches", C.c_uint64),
+                # ABI 3
+                ("rays_traced_total", C.c_uint64), ("frames_in_flight", C.c_uint64),
+                ("pipeline_slots", C.c_uint64), ("tlas_sah_splits", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

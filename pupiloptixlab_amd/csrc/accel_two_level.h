@@ -29,6 +29,7 @@ struct TwoLevelAccel {
     uint32_t *d_faces = nullptr;                     // BLAS primitives per instance (world records)
     uint32_t tlas_cap = 0, tlas_nodes = 0, num_nodes4 = 0, num_prims = 0;
     uint32_t tlas_depth = 0, blas_depth = 0;  // BVH4 levels (deepest BLAS); see kTraceStackEntries
+    uint32_t sah_splits = 0;  // TLAS splits of the last build chosen by the binned SAH (ranges > 1024 entries)
     // "world" mode (PUPIL_TL_MODE, default): every mesh instance gets a world-space copy of
     // its shape's BLAS (child boxes transformed and re-quantised conservatively) and the
     // TLAS is built over the nodes `braid` levels below each instance root, so the whole

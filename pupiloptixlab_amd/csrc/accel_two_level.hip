@@ -208,7 +208,9 @@ struct HostBox {
 };
 
 // Top-down SAH split of ids[b, e) (centroid sort on the widest axis, sweep).
-uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std::vector<HostBox> &boxes) {
+// binned (or null): counts the splits the binned SAH chose
+uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std::vector<HostBox> &boxes,
+                   uint32_t *binned) {
     HostBox cb = HostBox::empty();
     for (uint32_t i = b; i < e; i++) {
         const HostBox &x = boxes[ids[i]];
@@ -262,7 +264,10 @@ uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std
             const auto mid = std::stable_partition(ids.begin() + b, ids.begin() + e,
                                                    [&](uint32_t id) { return bin_of(id) < cut; });
             const uint32_t m = (uint32_t)(mid - ids.begin());
-            if (m > b && m < e) return m;
+            if (m > b && m < e) {
+                if (binned) (*binned)++;
+                return m;
+            }
         }
     }
     std::stable_sort(ids.begin() + b, ids.begin() + e, [&](uint32_t x, uint32_t y) {
@@ -293,16 +298,17 @@ uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std
 // links == nullptr: leaves are instances (object mode); else leaves are the entry
 // links themselves (world mode: nodes of the world BLAS copies, or records)
 int build_tlas_node(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std::vector<HostBox> &boxes,
-                    std::vector<Bvh4Node> &nodes, uint32_t level, uint32_t &depth, const std::vector<int> *links = nullptr) {
+                    std::vector<Bvh4Node> &nodes, uint32_t level, uint32_t &depth, const std::vector<int> *links = nullptr,
+                    uint32_t *binned = nullptr) {
     if (e - b == 1) return links ? (*links)[ids[b]] : make_leaf(ids[b], 1u);
     depth = std::max(depth, level + 1);
     uint32_t ranges[4][2];
     int nk = 0;
-    const uint32_t m = sah_split(ids, b, e, boxes);
+    const uint32_t m = sah_split(ids, b, e, boxes, binned);
     const uint32_t half[2][2] = {{b, m}, {m, e}};
     for (auto &h : half) {
         if (h[1] - h[0] > 1) {
-            const uint32_t mm = sah_split(ids, h[0], h[1], boxes);
+            const uint32_t mm = sah_split(ids, h[0], h[1], boxes, binned);
             ranges[nk][0] = h[0];
             ranges[nk++][1] = mm;
             ranges[nk][0] = mm;
@@ -325,7 +331,7 @@ int build_tlas_node(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const st
             clo[a][k] = cb.lo[a];
             chi[a][k] = cb.hi[a];
         }
-        link[k] = build_tlas_node(ids, ranges[k][0], ranges[k][1], boxes, nodes, level + 1, depth, links);
+        link[k] = build_tlas_node(ids, ranges[k][0], ranges[k][1], boxes, nodes, level + 1, depth, links, binned);
     }
     nodes[self] = encode_bvh4(nb.lo, nb.hi, clo, chi, link, nk);
     return (int)self;
@@ -518,8 +524,9 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
         std::vector<Bvh4Node> nodes;
         uint32_t depth = 0;
         int root = kTraverseDone;
+        uint32_t binned = 0;
         if (ids.size() == 1) root = links[0];
-        else if (!ids.empty()) root = build_tlas_node(ids, 0, (uint32_t)ids.size(), eb, nodes, 0u, depth, &links);
+        else if (!ids.empty()) root = build_tlas_node(ids, 0, (uint32_t)ids.size(), eb, nodes, 0u, depth, &links, &binned);
         if (nodes.size() > acc.tlas_cap) return -1;
         if (3u * depth + 3u * acc.blas_depth > (uint32_t)kTraceStackEntries) return -3;
         acc.tlas_depth = depth;
@@ -528,6 +535,7 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
                 hipSuccess)
             return -1;
         acc.tlas_nodes = (uint32_t)nodes.size();
+        acc.sah_splits = binned;
         acc.tlas_host = nodes;
         acc.root_link4 = (uint32_t)root;
         return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
@@ -542,9 +550,9 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
     for (uint32_t i = 0; i < n; i++)
         if (insts[i].kind == PUPIL_SHAPE_SPHERE || insts[i].blas_root != kTraverseDone) ids.push_back(i);
     std::vector<Bvh4Node> nodes;
-    uint32_t depth = 0;
-    const int root =
-        ids.empty() ? kTraverseDone : build_tlas_node(ids, 0, (uint32_t)ids.size(), boxes, nodes, 0u, depth);
+    uint32_t depth = 0, binned = 0;
+    const int root = ids.empty() ? kTraverseDone
+                                 : build_tlas_node(ids, 0, (uint32_t)ids.size(), boxes, nodes, 0u, depth, nullptr, &binned);
     if (nodes.size() > acc.tlas_cap) return -1;
     // a lane inside a BLAS holds the TLAS entries, the pending link + kReturnLink and the BLAS entries
     if (3u * depth + 2u + 3u * acc.blas_depth > (uint32_t)kTraceStackEntries) return -3;
@@ -554,6 +562,7 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
             hipSuccess)
         return -1;
     acc.tlas_nodes = (uint32_t)nodes.size();
+    acc.sah_splits = binned;
     acc.root_link4 = (uint32_t)root;
     return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
 }

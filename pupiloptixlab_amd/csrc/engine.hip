@@ -97,15 +97,30 @@ struct pupil_pt {
     uint32_t num_prims = 0;
     uint32_t leaf_size = 2;  // primitives per BVH leaf (PUPIL_LEAF_SIZE)
     bool mixed_trace = true;  // one persistent launch per bounce for shadow + extension rays (PUPIL_MIXED)
-    // Render-ahead (PUPIL_AHEAD): the last mixed launch of a render also traces the
-    // camera rays of the next render (seed + spp, same camera, tiling and batch), generated
-    // into the other half of the path-state buffers, so the next render starts at its
-    // first shade and the primary extend's launch tail is gone.  1 = single-spp renders
-    // (the PTPass::OnRun cadence, pt_pass.cpp:39-57), 2 = every render, 0 = off.
+    // Pipelined frames (render_pipelined, PUPIL_PIPE): the path state is a ring of K
+    // slots of one batch each; consecutive renders that continue each other (OnRun
+    // cadence, or PUPIL_HINT_CONTINUE) keep up to K frames in flight, each at its own
+    // bounce, and every iteration of a render advances all of them by one bounce in ONE
+    // persistent traversal launch and ONE shade launch.  A render returns with its own
+    // frame complete; the frames ahead of it depend only on (seed, camera, scene) and
+    // are dropped on any change.  ahead_mode: 1 = single-spp renders or the hint,
+    // 2 = every render, 0 = off (PUPIL_AHEAD).
     int ahead_mode = 1;
-    bool ahead_valid = false;
-    uint32_t ahead_seed = 0, ahead_spp = 0, ahead_local = 0, ahead_half = 0;
-    uint32_t ahead_key[5] = {0, 0, 0, 0, 0};
+    struct PipeFrame {
+        uint32_t slot, seed, phases;  // phases = bounces traced + shaded so far (complete at max_depth)
+        bool aov_scratch;             // shaded ahead of its render: AOVs wait in the slot's scratch
+    };
+    std::vector<PipeFrame> pipe;      // in flight, oldest first
+    uint32_t pipe_slots = 0;          // K of the ring in use
+    size_t pipe_np = 0;               // paths per slot
+    uint32_t pipe_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // w, h, tile size, rank, world, spp, depth, local pixels
+    uint32_t pipe_run = 0;            // consecutive renders that continued the previous one
+    uint32_t pipe_gen = 0;            // iterations so far (flags tags)
+    uint32_t pipe_limit = 0;          // PUPIL_PIPE: most slots (0 = max_depth)
+    double pipe_budget = 96e9;        // PUPIL_PIPE_GB: most HBM bytes for the ring's path state
+    bool pipe_valid = false;          // cleared by camera / instance / emitter updates
+    float *aov_scratch = nullptr;     // K slots x 7 floats per local pixel
+    size_t aov_cap = 0;
     hipStream_t last_stream = nullptr;  // of the last render (NULL = the default stream)
     bool rendered = false;
     double build_ms = 0.0;
@@ -121,13 +136,18 @@ struct pupil_pt {
     uint32_t pm_count = 0;
     // stats
     unsigned long long *trace_counters = nullptr;  // [0] nodes [1] prims
-    uint32_t *ray_log = nullptr;                   // per bounce: next, shadow
-    uint32_t last_paths = 0, last_bounces = 0;
+    uint32_t *ray_log = nullptr;                   // per iteration of the last render: next, shadow
+    uint32_t ray_log_cap = 0;                      // iterations it holds
+    unsigned long long *ray_cum = nullptr;         // device running totals: next, shadow rays
+    uint64_t primary_cum = 0;                      // host running total of camera rays
+    uint32_t last_paths = 0, last_iters = 0;
+    uint64_t last_primary = 0;
     bool last_stats = false;
     std::vector<hipEvent_t> trace_events;  // pairs
     std::vector<uint8_t> pair_kind;        // per pair: 0 extend, 1 shadow, 2 shade
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     uint32_t trace_pairs = 0;
+    bool pairs_keep = false;  // the pairs of PUPIL_STATS_TRACE_TIMING renders accumulate until read
     // PUPIL_TRACE_TAIL: per-wave start / drained / exit times of each traversal launch of a stats render
     unsigned long long *tail_buf = nullptr;
     uint32_t tail_waves = 0, tail_launches = 0;
@@ -170,11 +190,14 @@ struct pupil_pt {
         ps = PathState{};
         q.bins = q.nxsh = q.hist = nullptr;
         cap = 0;
-        ahead_valid = false;
+        pipe.clear();
+        pipe_valid = false;
     }
     ~pupil_pt() {
         (void)hipSetDevice(device);
         release_state();
+        if (aov_scratch) (void)hipFree(aov_scratch);
+        if (ray_log) (void)hipFree(ray_log);
         for (void *p : allocs) (void)hipFree(p);
         free_lbvh(bvh);
         free_two_level(tl);
@@ -375,12 +398,264 @@ uint32_t local_pixels(uint32_t w, uint32_t h, uint32_t ts, uint32_t rank, uint32
     return n;
 }
 
+// ------------------------------------------------------------------ frame schedules
+// Shared state of one pupil_pt_render call.
+struct RenderCtx {
+    pupil_pt *pt;
+    hipStream_t s;
+    bool stats, timing;
+    TraceStats ts_dev;
+    const uint32_t *key;  // w, h, tile size, rank, world
+    bool tail = false;
+    bool trace_only = false;  // PUPIL_STATS_TRACE_TIMING: traversal launches only
+    uint32_t pair = 0;
+    bool open = false;
+    const TraceStats *tsp() const { return stats ? &ts_dev : nullptr; }
+    // stage events only on request: each hipEventRecord between two kernels costs
+    // ~6 us of stream gap (9 per 1-spp render at D = 4)
+    void ev0(uint8_t kind) {
+        open = timing && !(trace_only && kind == 2);
+        if (!open) return;
+        pt->pair_kind[pair] = kind;
+        (void)hipEventRecord(pt->trace_events[2 * pair], s);
+    }
+    void ev1() {
+        if (!open) return;
+        (void)hipEventRecord(pt->trace_events[2 * pair + 1], s);
+        pair++;
+        open = false;
+    }
+    void tail_slot() {  // wave-time slice of the next traversal launch (PUPIL_TRACE_TAIL)
+        if (tail && pt->tail_launches < kMaxDepth + 1)
+            ts_dev.wave_times = pt->tail_buf + (size_t)pt->tail_launches++ * pt->tail_waves * 4;
+        else
+            ts_dev.wave_times = nullptr;
+    }
+    // path state of ring slot h: every array offset by h * paths
+    PathState view(uint32_t h, size_t paths) const {
+        PathState v = pt->ps;
+        const size_t o = (size_t)h * paths;
+        v.ray_o += o, v.ray_d += o, v.hit += o, v.thr += o, v.rad += o, v.misc += o;
+        v.sh_o += o, v.sh_d += o, v.sh_c += o, v.mbin += o, v.sflags += o;
+        return v;
+    }
+};
+
+// One batch rendered on its own: generate, primary extend, then per bounce shade,
+// flags partition and shadow + extension traversal, then accumulate.  Used by the
+// A/B traversal variants (BVH2 / BVH8 node formats, one ray per lane, PUPIL_MIXED=0).
+int render_classic(RenderCtx &cx, const FrameParams &fp) {
+    pupil_pt *pt = cx.pt;
+    hipStream_t s = cx.s;
+    pt->pipe.clear();
+    pt->pipe_valid = false;
+    int rc = ensure_state(pt, fp.num_paths);
+    if (rc) return rc;
+    const PathState ps = cx.view(0, fp.num_paths);
+    const uint32_t np = fp.num_paths;
+    Queues &q = pt->q;
+    auto bin_paths = [&]() {  // material bins of the traced paths -> q.bins (stable, increasing path id)
+        launch_partition(ps.mbin, np, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
+                         q.counts + kStartBins, q.counts + kScratch, nullptr, s);
+    };
+    const uint32_t interleave = pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u;
+    launch_generate(pt->sc, fp, ps, s);
+    cx.ev0(0);
+    cx.tail_slot();
+    // camera rays: the spp samples of a pixel on consecutive lanes (PUPIL_PRIMARY_ORDER=path: path order)
+    launch_extend(pt->sc, ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, cx.tsp(), s, interleave, fp.num_local);
+    cx.ev1();
+    if (!pt->shade_list) bin_paths();
+    const uint32_t bounces = fp.max_depth;
+    for (uint32_t b = 0; b < bounces; b++) {
+        const uint32_t tag = sflag_tag(fp.max_depth, b);
+        if (tag == 0) HIP_TRY(hipMemsetAsync(ps.sflags, 0, np, s));
+        cx.ev0(2);
+        launch_shade(pt->sc, fp, ps, q, tag, s, !pt->shade_list ? kShadeBins : (b == 0 ? kShadeAll : kShadeNext), 0u,
+                     np, np);
+        cx.ev1();
+        if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
+            // next (bit 0) and shadow (bit 1) lists -> q.nxsh, each in increasing path order
+            launch_partition(ps.sflags, np, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
+                             q.counts + kStartNext, nullptr, pt->ray_log + 2 * (b + 1), s, pt->ray_cum);
+            if (pt->mixed_trace && pt->sc.bvh_width >= 4 && pt->sc.trace_refill) {
+                cx.ev0(1);
+                cx.tail_slot();
+                launch_trace_mixed(pt->sc, ps, q, pt->ovf, pt->ovf_threads, cx.tsp(), s);
+                cx.ev1();
+            } else {
+                cx.ev0(1);
+                cx.tail_slot();
+                launch_shadow(pt->sc, ps, q, pt->ovf, pt->ovf_threads, cx.tsp(), s);
+                cx.ev1();
+                cx.ev0(0);
+                cx.tail_slot();
+                launch_extend(pt->sc, ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, cx.tsp(), s);
+                cx.ev1();
+            }
+            if (!pt->shade_list) bin_paths();
+        }
+    }
+    launch_accumulate(fp, ps, nullptr, false, s);
+    pt->last_iters = bounces;
+    pt->last_primary = np;
+    pt->primary_cum += np;
+    return PUPIL_OK;
+}
+
+// Pipelined frames.  The batch's path state is one slot of a ring of K slots.  A frame
+// runs max_depth phases -- phase b: trace (b = 0: the camera rays, else the shadow +
+// extension rays its bounce-(b-1) shade spawned) then the bounce-b shade -- and one
+// iteration of the loop below advances every frame in flight by one phase with one
+// flags partition over the ring, ONE persistent traversal launch (the listed shadow and
+// extension rays of all frames, plus the camera rays of a frame started in that
+// iteration) and ONE shade launch (each path at its own bounce).  A render runs the
+// iterations its own frame still needs and then accumulates it, so the frame is
+// complete when the call's work has run, as PTPass::OnRun requires
+// (pt_pass.cpp:51-56); the other frames in flight belong to the renders that continue
+// this one (random_seed + spp each, same camera, scene, tiling, spp and depth), and are
+// dropped when the next render does not continue it.  Frames are started in the last
+// run + 1 iterations of a render (run = renders in a row that continued the previous
+// one), so a continued sequence reaches one iteration per render after K renders, and
+// a render that is never continued (a moving camera) pays only for one frame's first
+// phase ahead.  Per path, every operation and its order are those of render_classic:
+// output is bit-identical.
+int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch *launch) {
+    pupil_pt *pt = cx.pt;
+    hipStream_t s = cx.s;
+    const uint32_t D = fp.max_depth;
+    const size_t np = fp.num_paths;
+    const bool may_pipe = pt->ahead_mode != 0 &&
+                          (pt->ahead_mode == 2 || launch->spp == 1 || (launch->hints & PUPIL_HINT_CONTINUE)) && !cx.stats &&
+                          D >= 2 && D <= 63;  // the 6-bit flags tags of a slot stay unambiguous for 63 iterations
+    uint32_t K = 1;
+    if (may_pipe) {
+        K = pt->pipe_limit ? std::min(pt->pipe_limit, D) : D;
+        constexpr double kPathBytes = 9 * 16 + 2 + 4 + 8 + 1;  // PathState + bins + nxsh + partition scratch
+        K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::floor(pt->pipe_budget / ((double)np * kPathBytes))));
+        while (K > 1 && (uint64_t)K * np >= (1ull << 31)) K--;
+    }
+    const uint32_t key[8] = {cx.key[0], cx.key[1], cx.key[2], cx.key[3], cx.key[4], fp.spp, D, fp.num_local};
+    bool reset = !(pt->pipe_valid && !pt->pipe.empty() && K == pt->pipe_slots && np == pt->pipe_np &&
+                   std::memcmp(key, pt->pipe_key, sizeof(key)) == 0 && pt->pipe.front().seed == launch->random_seed);
+    if ((size_t)K * np > pt->cap) {  // growing the ring loses its contents
+        reset = true;
+        int rc = ensure_state(pt, (size_t)K * np);
+        while (rc == PUPIL_ERR_OOM && K > 1) {  // a smaller ring, down to no frames ahead
+            K = K > 2 ? K / 2 : 1;
+            rc = ensure_state(pt, (size_t)K * np);
+        }
+        if (rc) return rc;
+    }
+    const uint32_t nl = fp.num_local;
+    if (K > 1 && (size_t)K * 7 * nl > pt->aov_cap) {
+        reset = true;
+        if (pt->aov_scratch) (void)hipFree(pt->aov_scratch);
+        pt->aov_scratch = nullptr;
+        pt->aov_cap = 0;
+        HIP_TRY(hipMalloc((void **)&pt->aov_scratch, sizeof(float) * (size_t)K * 7 * nl));
+        pt->aov_cap = (size_t)K * 7 * nl;
+    }
+    const PathState ring = pt->ps;
+    if (reset) {
+        pt->pipe.clear();
+        pt->pipe_run = 0;
+        pt->pipe_slots = K;
+        pt->pipe_np = np;
+        std::memcpy(pt->pipe_key, key, sizeof(key));
+        if (K > 1) {  // no stale flags / bins in slots this render does not start
+            HIP_TRY(hipMemsetAsync(ring.sflags, 0, (size_t)K * np, s));
+            if (!pt->shade_list) HIP_TRY(hipMemsetAsync(ring.mbin, 0xFF, (size_t)K * np, s));
+        }
+    } else {
+        pt->pipe_run++;
+    }
+    pt->pipe_valid = true;
+    Queues &q = pt->q;
+    const uint32_t nring = (uint32_t)((size_t)K * np);
+    const uint32_t interleave = pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u;
+    const uint32_t L = pt->pipe.empty() ? D : D - pt->pipe.front().phases;
+    auto scratch = [&](uint32_t slot) { return pt->aov_scratch + (size_t)slot * 7 * nl; };
+    uint64_t started = 0;
+    for (uint32_t it = 0; it < L; it++) {
+        const bool had = !pt->pipe.empty();
+        // start a frame: this render's own on an empty pipeline, else the next one ahead
+        // in the last run + 1 iterations while a slot is free
+        const bool inject = !had || (pt->pipe.size() < K && it + pt->pipe_run + 1 >= L);
+        pupil_pt::PipeFrame nf{0u, launch->random_seed, 0u, false};
+        if (inject) {
+            if (had) {
+                nf.slot = (pt->pipe.back().slot + 1) % K;
+                nf.seed = pt->pipe.back().seed + fp.spp;
+                nf.aov_scratch = true;  // completes in a later render
+            }
+            FrameParams fg = fp;
+            fg.seed0 = nf.seed;
+            launch_generate(pt->sc, fg, cx.view(nf.slot, np), s);
+            started++;
+        }
+        if (had) {
+            // the rays the previous iteration's shade spawned, over the whole ring, in
+            // increasing path id: next (bit 0) and shadow (bit 1) lists -> q.nxsh
+            const uint32_t tag = pt->pipe_gen % 63u + 1u;
+            launch_partition(ring.sflags, nring, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
+                             q.counts + kStartNext, nullptr, pt->ray_log + 2 * it, s, pt->ray_cum);
+            cx.ev0(1);
+            cx.tail_slot();
+            if (inject)  // + the new frame's camera rays, dequeued first in every chunk (pixel-major)
+                launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s, (uint32_t)np, 0u,
+                                   (uint32_t)(nf.slot * np), interleave, nl);
+            else
+                launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s);
+            cx.ev1();
+        } else {
+            cx.ev0(0);
+            cx.tail_slot();
+            launch_extend(pt->sc, cx.view(nf.slot, np), q, nullptr, nullptr, (uint32_t)np, pt->ovf, pt->ovf_threads,
+                          cx.tsp(), s, interleave, nl);
+            cx.ev1();
+        }
+        if (!pt->shade_list)  // material bins of every path traced in this iteration -> q.bins
+            launch_partition(ring.mbin, nring, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
+                             q.counts + kStartBins, q.counts + kScratch, nullptr, s);
+        FrameParams fs = fp;
+        if (inject && nf.aov_scratch) {  // AOVs of a frame ahead wait in its slot's scratch
+            fs.albedo = scratch(nf.slot);
+            fs.normal = fs.albedo + 3 * (size_t)nl;
+            fs.test = fs.albedo + 6 * (size_t)nl;
+            fs.aov_local = 1;
+        }
+        if (D > 63) HIP_TRY(hipMemsetAsync(ring.sflags, 0, nring, s));  // K = 1: tags would alias
+        const uint32_t wtag = (pt->pipe_gen + 1u) % 63u + 1u;
+        const ShadeList list = !pt->shade_list ? kShadeBins : (had ? (inject ? kShadeNextRange : kShadeNext) : kShadeAll);
+        const uint32_t max_count = (uint32_t)std::min<uint64_t>(
+            nring, (had ? (uint64_t)pt->pipe.size() * np : 0u) + (inject ? np : 0u));
+        cx.ev0(2);
+        launch_shade(pt->sc, fs, ring, q, wtag, s, list, (uint32_t)(nf.slot * np), inject ? (uint32_t)np : 0u, max_count);
+        cx.ev1();
+        pt->pipe_gen++;
+        for (auto &f : pt->pipe) f.phases++;
+        if (inject) {
+            nf.phases = 1;
+            pt->pipe.push_back(nf);
+        }
+    }
+    // this render's frame is complete: accumulate it and free its slot
+    const pupil_pt::PipeFrame f = pt->pipe.front();
+    pt->pipe.erase(pt->pipe.begin());
+    launch_accumulate(fp, cx.view(f.slot, np), f.aov_scratch ? scratch(f.slot) : nullptr, K > 1, s);
+    pt->last_iters = L;
+    pt->last_primary = started * np;
+    pt->primary_cum += started * np;
+    return PUPIL_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 const char *pupil_last_error(void) { return g_last_error.c_str(); }
-int pupil_abi_version(void) { return 2; }
+int pupil_abi_version(void) { return 3; }
 
 int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank, uint32_t tile_world,
                           uint32_t *out_pixels, uint32_t *inout_count) {
@@ -614,6 +889,8 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
     if (const char *a = std::getenv("PUPIL_AHEAD")) pt->ahead_mode = std::min(2, std::max(0, std::atoi(a)));
+    if (const char *k = std::getenv("PUPIL_PIPE")) pt->pipe_limit = (uint32_t)std::min(63, std::max(0, std::atoi(k)));
+    if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     sc.prim_inst = d_prim_inst;
@@ -624,10 +901,11 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     // traversal overflow stacks, counters, events
     pt->ovf_threads = trace_grid_blocks() * (uint32_t)kTraceBlock;
     if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 32) ||
-        pt->alloc(&pt->ray_log, 2 * 130) || pt->alloc(&pt->q.counts, kCountSlots) ||
+        pt->alloc(&pt->ray_cum, 2) || pt->alloc(&pt->q.counts, kCountSlots) ||
         pt->alloc(&pt->q.work, kWorkSlots))
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
-    if (hipMemset(pt->q.work, 0, kWorkSlots * sizeof(uint32_t)) != hipSuccess)
+    if (hipMemset(pt->q.work, 0, kWorkSlots * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(pt->ray_cum, 0, 2 * sizeof(unsigned long long)) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "workspace clear failed"));
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
@@ -647,7 +925,7 @@ int pupil_pt_set_camera(pupil_pt *pt, const float sample_to_camera[16], const fl
     if (!pt || !sample_to_camera || !camera_to_world) return fail(PUPIL_ERR_INVALID, "null argument");
     if (std::memcmp(pt->sc.camera.s2c, sample_to_camera, sizeof(pt->sc.camera.s2c)) != 0 ||
         std::memcmp(pt->sc.camera.c2w, camera_to_world, sizeof(pt->sc.camera.c2w)) != 0)
-        pt->ahead_valid = false;  // the render-ahead camera rays belong to the old view
+        pt->pipe_valid = false;  // frames in flight were started with the old view
     std::memcpy(pt->sc.camera.s2c, sample_to_camera, sizeof(pt->sc.camera.s2c));
     std::memcpy(pt->sc.camera.c2w, camera_to_world, sizeof(pt->sc.camera.c2w));
     return PUPIL_OK;
@@ -662,7 +940,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     if (instance >= pt->h_insts.size()) return fail(PUPIL_ERR_INVALID, "instance index out of range");
     HIP_TRY(hipSetDevice(pt->device));
     HIP_TRY(hipDeviceSynchronize());  // no render may still read the old tables
-    pt->ahead_valid = false;          // render-ahead hits were traced against the old geometry
+    pt->pipe_valid = false;           // frames in flight were traced against the old geometry
     DevInstance &d = pt->h_insts[instance];
     std::memcpy(d.to_world, to_world, sizeof(d.to_world));
     std::memcpy(d.to_object, to_object, sizeof(d.to_object));
@@ -724,17 +1002,13 @@ int pupil_pt_update_emitters(pupil_pt *pt, const pupil_scene_desc *scene) {
     if (scene->num_area_emitters && !scene->area_emitters) return fail(PUPIL_ERR_INVALID, "missing emitter array");
     HIP_TRY(hipSetDevice(pt->device));
     HIP_TRY(hipDeviceSynchronize());
-    pt->ahead_valid = false;
+    pt->pipe_valid = false;
     return upload_emitters(pt, scene);
 }
 
 int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_launch *launch, void *hip_stream) {
     if (!pt || !out || !launch || !out->accum) return fail(PUPIL_ERR_INVALID, "null argument");
     if (launch->spp == 0) return PUPIL_OK;
-    // PTPass clamps the inspector's max_depth to 1..128 (pt_pass.cpp:225-237); the
-    // per-bounce ray log and the stage-event list are sized for that range
-    if ((launch->max_depth ? launch->max_depth : pt->max_depth) > kMaxDepth)
-        return fail(PUPIL_ERR_INVALID, "max_depth above 128");
     const uint32_t world = launch->tile_world ? launch->tile_world : 1u;
     const uint32_t ts = launch->tile_size ? launch->tile_size : 32u;
     if (launch->tile_rank >= world) return fail(PUPIL_ERR_INVALID, "tile_rank >= tile_world");
@@ -769,31 +1043,11 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     if (paths >= (1ull << 31)) return fail(PUPIL_ERR_UNSUPPORTED, "too many paths in one batch");
     const bool stats = (launch->collect_stats & PUPIL_STATS_COUNTERS) != 0;
     const bool timing = (launch->collect_stats & PUPIL_STATS_TIMING) != 0;
-    const uint32_t depth = launch->max_depth ? launch->max_depth : pt->max_depth;
-    // render-ahead: use the camera rays the previous render traced for this one, and
-    // trace the next render's in this one's last mixed launch (BVH4 persistent kernels;
-    // counter renders keep their own primary launch so the counters stay per render)
-    const bool use_ahead = pt->ahead_valid && !stats && launch->random_seed == pt->ahead_seed && launch->spp == pt->ahead_spp &&
-                           num_local == pt->ahead_local && std::memcmp(key, pt->ahead_key, sizeof(key)) == 0;
-    const bool make_ahead = pt->ahead_mode != 0 &&
-                            (pt->ahead_mode == 2 || launch->spp == 1 || (launch->hints & PUPIL_HINT_CONTINUE)) && !stats &&
-                            depth >= 2 && pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill != 0 &&
-                            paths < (1ull << 30);
-    pt->ahead_valid = false;
+    // The reference takes integrator.max_depth unclamped at SetScene (pt_pass.cpp:112-115;
+    // only the inspector clamps to 1..128): any depth renders.  Diagnostics sized per
+    // bounce (tail buffer) cover the first kMaxDepth launches.
+    const uint32_t depth = std::max(1u, launch->max_depth ? launch->max_depth : pt->max_depth);
     if (pt->rendered && s != pt->last_stream) HIP_TRY(hipStreamWaitEvent(s, pt->ev_end, 0));
-    const size_t cap_before = pt->cap;
-    int rc = ensure_state(pt, paths * (use_ahead || make_ahead ? 2 : 1));
-    if (rc) return rc;
-    const uint32_t half = use_ahead && pt->cap == cap_before ? pt->ahead_half : 0u;
-    const bool ahead_in = use_ahead && pt->cap == cap_before;
-    auto view = [&](uint32_t h) {  // path state of half h: every array offset by h * paths
-        PathState v = pt->ps;
-        const size_t o = (size_t)h * paths;
-        v.ray_o += o, v.ray_d += o, v.hit += o, v.thr += o, v.rad += o, v.misc += o;
-        v.sh_o += o, v.sh_d += o, v.sh_c += o, v.mbin += o, v.sflags += o;
-        return v;
-    };
-    const PathState ps = view(half);
 
     FrameParams fp{};
     fp.width = pt->width;
@@ -804,8 +1058,9 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     fp.seed0 = launch->random_seed;
     fp.cnt0 = launch->sample_cnt;
     fp.accumulate = launch->accumulate;
-    fp.max_depth = launch->max_depth ? launch->max_depth : pt->max_depth;
+    fp.max_depth = depth;
     fp.compact = out->compact;
+    fp.aov_local = out->compact;
     fp.pixel_map = map;
     fp.accum = (float4 *)out->accum;
     fp.frame = (float4 *)out->frame;
@@ -814,117 +1069,51 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     fp.test = (float *)out->test;
     fp.nee_count = stats ? pt->trace_counters + 16 : nullptr;
 
-    TraceStats ts_dev{pt->trace_counters};
-    const TraceStats *tsp = stats ? &ts_dev : nullptr;
+    // PUPIL_STATS_TRACE_TIMING: events around the traversal launches only, summed over
+    // every render since pupil_pt_stats last read them (a timed sequence of renders)
+    const bool trace_timing = (launch->collect_stats & PUPIL_STATS_TRACE_TIMING) != 0 && !timing;
+    RenderCtx cx{pt, s, stats, timing || trace_timing, TraceStats{pt->trace_counters}, key};
+    cx.trace_only = trace_timing;
+    cx.pair = trace_timing && pt->pairs_keep ? pt->trace_pairs : 0u;
+    pt->pairs_keep = trace_timing;
     const bool tail = stats && std::getenv("PUPIL_TRACE_TAIL");
     if (tail && !pt->tail_buf) {
         pt->tail_waves = pt->ovf_threads / 64u;
         if (pt->alloc(&pt->tail_buf, (size_t)(kMaxDepth + 1) * pt->tail_waves * 4)) return fail(PUPIL_ERR_OOM, "tail buffer");
     }
     if (tail) HIP_TRY(hipMemsetAsync(pt->tail_buf, 0, sizeof(unsigned long long) * (kMaxDepth + 1) * pt->tail_waves * 4, s));
+    cx.tail = tail;
     pt->tail_launches = 0;
-    auto tail_slot = [&]() {  // wave-time slice of the next traversal launch
-        if (tail) ts_dev.wave_times = pt->tail_buf + (size_t)pt->tail_launches++ * pt->tail_waves * 4;
-    };
-    const uint32_t bounces = fp.max_depth;
-    // events: begin/end + one pair per stage launch (kind 0 extend, 1 shadow, 2 shade)
-    const uint32_t pairs_needed = 3 * bounces + 1;
+    const uint32_t iters = depth + 1;  // both schedules run at most depth iterations (+1 spare)
+    if (iters > pt->ray_log_cap) {
+        if (pt->ray_log) (void)hipFree(pt->ray_log);
+        pt->ray_log = nullptr;
+        pt->ray_log_cap = 0;
+        HIP_TRY(hipMalloc((void **)&pt->ray_log, sizeof(uint32_t) * 2 * iters));
+        pt->ray_log_cap = iters;
+    }
+    HIP_TRY(hipMemsetAsync(pt->ray_log, 0, sizeof(uint32_t) * 2 * iters, s));
+    // events: begin/end + one pair per stage launch (kind 0 primary extend, 1 bounce trace, 2 shade)
+    const uint32_t pairs_needed = cx.pair + 3 * depth + 1;
     while (pt->trace_events.size() < 2 * pairs_needed) {
         hipEvent_t e;
         HIP_TRY(hipEventCreate(&e));
         pt->trace_events.push_back(e);
     }
-    pt->pair_kind.assign(pairs_needed, 0);
-    uint32_t pair = 0;
-    // stage events only on request: each hipEventRecord between two kernels costs
-    // ~6 us of stream gap (9 per 1-spp render at D = 4)
-    auto ev0 = [&](uint8_t kind) {
-        if (!timing) return;
-        pt->pair_kind[pair] = kind;
-        (void)hipEventRecord(pt->trace_events[2 * pair], s);
-    };
-    auto ev1 = [&]() {
-        if (!timing) return;
-        (void)hipEventRecord(pt->trace_events[2 * pair + 1], s);
-        pair++;
-    };
+    pt->pair_kind.resize(pairs_needed, 0);
 
     HIP_TRY(hipEventRecord(pt->ev_begin, s));
     if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 32 * sizeof(unsigned long long), s));
-    const uint32_t np = fp.num_paths;
-    Queues &q = pt->q;
-    // material bins of the traced paths -> q.bins (stable, increasing path id)
-    auto bin_paths = [&]() {
-        launch_partition(ps.mbin, np, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
-                         q.counts + kStartBins, q.counts + kScratch, nullptr, s);
-    };
-    // No per-stage clears: the primary extend writes every path's material bin,
-    // each shade writes its paths' flags (with the bounce tag) and resets their
-    // bin to 0xFF, the persistent kernels reset their own work heads, and the
-    // flags partition logs the per-bounce ray counts.
-    const uint32_t interleave = pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u;
-    if (!ahead_in) {  // else the previous render traced this one's camera rays (render-ahead)
-        launch_generate(pt->sc, fp, ps, s);
-        ev0(0);
-        tail_slot();
-        // camera rays: the spp samples of a pixel on consecutive lanes (PUPIL_PRIMARY_ORDER=path: path order)
-        launch_extend(pt->sc, ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, tsp, s, interleave, fp.num_local);
-        ev1();
-    }
-    if (!pt->shade_list) bin_paths();
-    for (uint32_t b = 0; b < bounces; b++) {
-        const uint32_t tag = sflag_tag(fp.max_depth, b);
-        if (tag == 0) HIP_TRY(hipMemsetAsync(ps.sflags, 0, np, s));
-        ev0(2);
-        launch_shade(pt->sc, fp, ps, q, b, s, !pt->shade_list ? kShadeBins : (b == 0 ? kShadeAll : kShadeNext));
-        ev1();
-        if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
-            // next (bit 0) and shadow (bit 1) lists -> q.nxsh, each in increasing path order
-            // (grouping the next list by direction octant measured slower: 21.2 vs 20.8 ms extend)
-            launch_partition(ps.sflags, np, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
-                             q.counts + kStartNext, nullptr, b < 128 ? pt->ray_log + 2 * b : nullptr, s);
-            if (pt->mixed_trace && pt->sc.bvh_width >= 4 && pt->sc.trace_refill) {
-                // render-ahead: the last mixed launch also traces the next render's camera rays,
-                // generated into the other half of the buffers (seed + spp, this camera and tiling)
-                const bool ahead_out = make_ahead && b + 2 == bounces;
-                if (ahead_out) {
-                    FrameParams fa = fp;
-                    fa.seed0 = fp.seed0 + fp.spp;
-                    launch_generate(pt->sc, fa, view(half ^ 1u), s);
-                }
-                ev0(1);
-                tail_slot();
-                if (ahead_out)  // addressed from the base of both halves (offsets stay non-negative)
-                    launch_trace_mixed(pt->sc, pt->ps, q, pt->ovf, pt->ovf_threads, tsp, s, np, half * np,
-                                       (half ^ 1u) * np, interleave, fp.num_local);
-                else
-                    launch_trace_mixed(pt->sc, ps, q, pt->ovf, pt->ovf_threads, tsp, s);
-                ev1();
-                if (ahead_out) {
-                    pt->ahead_valid = true;
-                    pt->ahead_seed = fp.seed0 + fp.spp;
-                    pt->ahead_spp = fp.spp;
-                    pt->ahead_local = num_local;
-                    pt->ahead_half = half ^ 1u;
-                    std::memcpy(pt->ahead_key, key, sizeof(key));
-                }
-            } else {
-                ev0(1);
-                launch_shadow(pt->sc, ps, q, pt->ovf, pt->ovf_threads, tsp, s);
-                ev1();
-                ev0(0);
-                launch_extend(pt->sc, ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, tsp, s);
-                ev1();
-            }
-            if (!pt->shade_list) bin_paths();
-        }
-    }
-    launch_accumulate(fp, ps, s);
+    // the persistent BVH4 kernels with mixed extension + shadow launches pipeline frames;
+    // the A/B traversal variants (BVH2 / BVH8 node formats, one ray per lane, separate
+    // shadow and extension launches) render each batch on its own
+    const bool pipelined = pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill != 0;
+    const int rc = pipelined ? render_pipelined(cx, fp, launch) : render_classic(cx, fp);
+    if (rc) return rc;
     HIP_TRY(hipEventRecord(pt->ev_end, s));
     HIP_TRY(hipGetLastError());
-    pt->trace_pairs = pair;
+    pt->trace_pairs = cx.pair;
     pt->last_paths = fp.num_paths;
-    pt->last_bounces = bounces < 129 ? bounces : 129;  // rays are logged for bounces 0..127
     pt->last_stats = stats;
     pt->last_stream = s;
     pt->rendered = true;
@@ -936,14 +1125,25 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
     HIP_TRY(hipSetDevice(pt->device));
     HIP_TRY(hipEventSynchronize(pt->ev_end));
     pupil_pt_counters c = pt->totals;
+    {
+        unsigned long long cum[2] = {0, 0};
+        HIP_TRY(hipMemcpy(cum, pt->ray_cum, sizeof(cum), hipMemcpyDeviceToHost));
+        c.rays_traced_total = pt->primary_cum + cum[0] + cum[1];
+        c.frames_in_flight = pt->pipe.size();
+        c.pipeline_slots = pt->pipe_slots;
+        c.tlas_sah_splits = pt->two_level ? pt->tl.sah_splits : 0u;
+    }
     if (pt->last_paths) {
-        std::vector<uint32_t> log(2 * 130, 0);
-        HIP_TRY(hipMemcpy(log.data(), pt->ray_log, sizeof(uint32_t) * log.size(), hipMemcpyDeviceToHost));
-        c.primary_rays = pt->last_paths;
+        // rays traced by the last render's launches (pipelined renders: of every frame in
+        // flight; iteration 0 of a render that started on an empty pipeline logs none)
+        std::vector<uint32_t> log(2 * (size_t)pt->last_iters, 0);
+        if (!log.empty())
+            HIP_TRY(hipMemcpy(log.data(), pt->ray_log, sizeof(uint32_t) * log.size(), hipMemcpyDeviceToHost));
+        c.primary_rays = pt->last_primary;
         c.path_samples = pt->last_paths;
         c.extension_rays = 0;
         c.shadow_rays = 0;
-        for (uint32_t b = 0; b + 1 < pt->last_bounces; b++) {  // the last bounce spawns no rays
+        for (uint32_t b = 0; b < pt->last_iters; b++) {
             c.extension_rays += log[2 * b];
             c.shadow_rays += log[2 * b + 1];
         }
@@ -958,6 +1158,7 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
             kind_ms[pt->pair_kind[i]] += m;
             kind_n[pt->pair_kind[i]]++;
         }
+        pt->pairs_keep = false;  // read: the next PUPIL_STATS_TRACE_TIMING render starts a new sum
         c.trace_ms = kind_ms[0] + kind_ms[1];
         c.trace_launches = kind_n[0] + kind_n[1];
         c.extend_ms = kind_ms[0];

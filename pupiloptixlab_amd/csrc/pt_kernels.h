@@ -39,7 +39,7 @@ struct PathState {
     float4 *hit;        // t, b1, b2, sorted primitive index (bits) or kMissIndex
     float4 *thr;        // xyz throughput, w = pdf of the BSDF sample that spawned the ray
     float4 *rad;        // xyz radiance
-    uint4 *misc;        // x rng, y bounce | delta<<8, z/w texcoord (stale semantics, geometry.h:298-304)
+    uint4 *misc;        // x rng, y bounce (bits 0..23) | delta << 31, z/w texcoord (stale semantics, geometry.h:298-304)
     float4 *sh_o;       // shadow ray origin, w = tmax
     float4 *sh_d;       // shadow ray direction
     float4 *sh_c;       // pending NEE contribution
@@ -104,6 +104,9 @@ struct FrameParams {
     float *normal;
     float *test;
     unsigned long long *nee_count;  // collect_stats: paths that reached the shadow test (main.cu:113-123)
+    // shade: the AOV pointers above are indexed by the local pixel (compact output, or the
+    // per-slot AOV scratch of a frame that completes in a later render); else by y*w+x
+    uint32_t aov_local;
 };
 
 struct TraceStats {
@@ -122,11 +125,16 @@ void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathSta
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
                    const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
                    const TraceStats *stats, hipStream_t s, uint32_t interleave_spp = 0, uint32_t num_local = 0);
-// which paths a shade launch walks: the material-bin partition (q.bins), every path
-// (after the primary extend), or the previous bounce's next list (q.nxsh)
-enum ShadeList : int { kShadeBins = 0, kShadeAll = 1, kShadeNext = 2 };
-void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,
-                  uint32_t bounce, hipStream_t s, ShadeList list = kShadeBins);
+// which paths a shade launch walks: the material-bin partition (q.bins), a range of path
+// ids (every path of a batch after its primary extend), the previous bounce's next list
+// (q.nxsh), or that next list followed by a range (pipelined frames: the extension rays of
+// the frames in flight, then the camera rays of the frame started in the same launch).
+// Each path's bounce is read from its state (PathState::misc.y), so one launch may shade
+// paths of several frames at different bounces; `tag` is the bounce tag the launch writes
+// into the flags bytes (sflag_tag, or the pipeline's generation tag).
+enum ShadeList : int { kShadeBins = 0, kShadeAll = 1, kShadeNext = 2, kShadeNextRange = 3 };
+void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q, uint32_t tag,
+                  hipStream_t s, ShadeList list, uint32_t range_base, uint32_t range_n, uint32_t max_count);
 void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                    const TraceStats *stats, hipStream_t s);
 // one persistent launch over the next + shadow lists of a bounce (BVH4 persistent path only)
@@ -138,7 +146,11 @@ void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, 
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                         const TraceStats *stats, hipStream_t s, uint32_t ahead_count = 0, uint32_t list_base = 0,
                         uint32_t ahead_base = 0, uint32_t ahead_spp = 0, uint32_t ahead_local = 0);
-void launch_accumulate(const FrameParams &fp, const PathState &ps, hipStream_t s);
+// running mean of the batch's frames into fp.accum / fp.frame; aov_src (or null): the
+// frame's AOVs from the slot scratch (3n albedo, 3n normal, n test floats) copied to the
+// outputs; clear_flags: zero the frame's flags bytes (its ring slot is free again)
+void launch_accumulate(const FrameParams &fp, const PathState &ps, const float *aov_src, bool clear_flags,
+                       hipStream_t s);
 uint32_t trace_grid_blocks();
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
                         uint32_t ovf_threads, uint32_t *work, hipStream_t s);
@@ -148,9 +160,11 @@ void launch_debug_select(const DeviceScene &sc, const float *p, int *out, uint32
 
 // stable partition of path ids 0..n-1 by a key byte (queue_partition.hip)
 uint32_t partition_hist_entries(uint32_t n);
+// log_out (or null): the nbins counts; cum_out (or null): the counts are added to these
+// nbins running 64-bit totals (rays traced since the engine was created)
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
                       uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, uint32_t *log_out,
-                      hipStream_t s);
+                      hipStream_t s, unsigned long long *cum_out = nullptr);
 
 // LBVH builder (bvh_build.hip)
 struct BvhBuildInput {

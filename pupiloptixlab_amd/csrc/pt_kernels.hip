@@ -1497,19 +1497,26 @@ __device__ __forceinline__ const DevEmitter *select_emitter(const DeviceScene &s
 // One path that hit a surface of material MAT (0 = unknown type): emission and
 // MIS at the hit, loop head, NEE sample, BSDF sample (main.cu:84-163).
 // Returns the next/shadow flags byte (bit 0 extension ray, bit 1 shadow ray).
+// p: path id (in a pipelined ring: slot * num_paths + sample * num_local + local pixel);
+// misc: its PathState::misc record (bounce in y), already loaded by the launch.
+// Last sample of its frame, and the local pixel (AOVs are written for the last sample).
+__device__ __forceinline__ bool last_sample(const FrameParams &fp, uint32_t p, uint32_t &l) {
+    const uint32_t q = p / fp.num_local;
+    l = p - q * fp.num_local;
+    return q % fp.spp + 1u == fp.spp;
+}
+
 template <uint32_t MAT>
 __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
-                                              uint32_t p, uint32_t bounce) {
+                                              uint32_t p, uint4 misc) {
     bool push_next = false, push_shadow = false;
-    const uint32_t s = p / fp.num_local;
-    const uint32_t l = p - s * fp.num_local;
     const float4 h = ps.hit[p];
     const float4 o4 = ps.ray_o[p];
     const float4 d4 = ps.ray_d[p];
     const vec3 ray_o = f3(o4), ray_d = f3(d4);
-    uint4 misc = ps.misc[p];
     uint32_t rng = misc.x;
     const uint32_t flags = misc.y;
+    const uint32_t bounce = flags & 0xFFFFFFu;
     float4 thr4 = ps.thr[p];
     vec3 T = f3(thr4);
     const float prev_pdf = thr4.w;
@@ -1529,8 +1536,9 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     if (bounce == 0) {
         if (hg.emitter >= 0) L = L + emitter_radiance(sc.areas[hg.emitter], geo.texcoord);  // main.cu:88-92
         const float test = rng_next(rng);                                                    // main.cu:101
-        if (s + 1 == fp.spp) {
-            const uint32_t out = fp.compact ? l : global_pixel(fp, l);
+        uint32_t l;
+        if (last_sample(fp, p, l)) {
+            const uint32_t out = fp.aov_local ? l : global_pixel(fp, l);
             if (fp.albedo) {
                 const vec3 al = bsdf_albedo(bsdf);
                 fp.albedo[3 * out + 0] = al.x;
@@ -1550,7 +1558,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         float pdf_e;
         emitter_eval_area(e, geo, ray_o, Le, pdf_e);
         if (!is_zero(pdf_e)) {
-            const float mis = (flags >> 8) & 1u ? 1.f : mis_weight(prev_pdf, pdf_e * e.select_probability);
+            const float mis = (flags >> 31) ? 1.f : mis_weight(prev_pdf, pdf_e * e.select_probability);
             L = L + T * Le * mis;
         }
     }
@@ -1616,7 +1624,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     }
     ps.thr[p] = f4(T, pdf_b);
     ps.rad[p] = f4(L, 0.f);
-    ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 8), __float_as_uint(geo.texcoord.x),
+    ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
                             __float_as_uint(geo.texcoord.y));
     return (push_next ? 1u : 0u) | (push_shadow ? 2u : 0u) | (nee ? 4u : 0u);
 }
@@ -1624,13 +1632,11 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
 // Paths whose ray left the scene (__miss__default, main.cu:196-212, and the
 // env handling at main.cu:87-99 / 165-169).
 __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
-                                           uint32_t p, uint32_t bounce) {
-    if (bounce == 0) {
-        const uint32_t s = p / fp.num_local;
-        const uint32_t l = p - s * fp.num_local;
+                                           uint32_t p, uint4 misc) {
+    if ((misc.y & 0xFFFFFFu) == 0u) {
         float4 rad4 = ps.rad[p];
         vec3 L = f3(rad4);
-        uint32_t rng = ps.misc[p].x;
+        uint32_t rng = misc.x;
         if (sc.has_env) {
             vec3 Le;
             float pdf;
@@ -1638,8 +1644,9 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
             L = L + Le;  // main.cu:185, no MIS on the camera ray
         }
         const float test = rng_next(rng);
-        if (s + 1 == fp.spp) {
-            const uint32_t out = fp.compact ? l : global_pixel(fp, l);
+        uint32_t l;
+        if (last_sample(fp, p, l)) {
+            const uint32_t out = fp.aov_local ? l : global_pixel(fp, l);
             if (fp.albedo) fp.albedo[3 * out] = fp.albedo[3 * out + 1] = fp.albedo[3 * out + 2] = 0.f;
             if (fp.normal) fp.normal[3 * out] = fp.normal[3 * out + 1] = fp.normal[3 * out + 2] = 0.f;
             if (fp.test) fp.test[out] = test;
@@ -1663,22 +1670,24 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
 // branch below is wave-uniform almost everywhere.  One launch instead of nine
 // per bounce keeps empty-bin launches off the frame (they cost ~4 us each).
 // SHADE_LIST (single-material scenes, ShadeList): no material partition; the launch
-// walks the paths the last traversal traced -- all paths after the primary extend,
-// else the previous bounce's next list, both in increasing path order -- and takes
-// each path's bin from the byte the traversal wrote.  Only the miss / hit split
-// diverges inside a wave, which costs less than the three partition launches.
+// walks the paths the last traversal traced -- a range of path ids after a primary
+// extend, the previous bounce's next list, or both (pipelined frames) -- in increasing
+// path order, and takes each path's bin from the hit (or the byte the traversal wrote).
+// Only the miss / hit split diverges inside a wave, which costs less than the three
+// partition launches.  Each path's bounce comes from its own state, so the paths of
+// several frames in flight (pipelined renders, engine.hip) share one launch.
 template <int LIST>
 __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
-                                                           uint32_t bounce) {
+                                                           uint32_t tag, uint32_t range_base, uint32_t range_n) {
+    const uint32_t n_list = LIST == kShadeNext || LIST == kShadeNextRange ? q.counts[kCntNext] : 0u;
     const uint32_t count = LIST == kShadeBins ? q.counts[kScratch]  // all traced paths (total of the bin partition)
-                                              : (LIST == kShadeAll ? fp.num_paths : q.counts[kCntNext]);
-    const uint32_t tag = sflag_tag(fp.max_depth, bounce);
+                                              : n_list + (LIST == kShadeAll || LIST == kShadeNextRange ? range_n : 0u);
     uint32_t start[kPartMaxBins];
 #pragma unroll
     for (int b = 0; b < kPartMaxBins; b++) start[b] = LIST == kShadeBins ? q.counts[kStartBins + b] : 0u;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
-        const uint32_t p = LIST == kShadeBins ? q.bins[i] : (LIST == kShadeAll ? i : q.nxsh[i]);
+        const uint32_t p = LIST == kShadeBins ? q.bins[i] : (i < n_list ? q.nxsh[i] : range_base + (i - n_list));
         // bin of list position i: the last bin starting at or before i (an empty
         // bin starts where the next one does, so it is never the last such bin)
         uint32_t bin = 0;
@@ -1690,17 +1699,18 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, Frame
         } else {
             bin = ps.mbin[p];
         }
+        const uint4 misc = ps.misc[p];
         uint32_t flags = 0;
         switch (bin) {
-        case 0: shade_miss(sc, fp, ps, p, bounce); break;
-        case PUPIL_MAT_DIFFUSE: flags = shade_hit<PUPIL_MAT_DIFFUSE>(sc, fp, ps, p, bounce); break;
-        case PUPIL_MAT_DIELECTRIC: flags = shade_hit<PUPIL_MAT_DIELECTRIC>(sc, fp, ps, p, bounce); break;
-        case PUPIL_MAT_ROUGH_DIELECTRIC: flags = shade_hit<PUPIL_MAT_ROUGH_DIELECTRIC>(sc, fp, ps, p, bounce); break;
-        case PUPIL_MAT_CONDUCTOR: flags = shade_hit<PUPIL_MAT_CONDUCTOR>(sc, fp, ps, p, bounce); break;
-        case PUPIL_MAT_ROUGH_CONDUCTOR: flags = shade_hit<PUPIL_MAT_ROUGH_CONDUCTOR>(sc, fp, ps, p, bounce); break;
-        case PUPIL_MAT_PLASTIC: flags = shade_hit<PUPIL_MAT_PLASTIC>(sc, fp, ps, p, bounce); break;
-        case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p, bounce); break;
-        default: flags = shade_hit<0u>(sc, fp, ps, p, bounce); break;
+        case 0: shade_miss(sc, fp, ps, p, misc); break;
+        case PUPIL_MAT_DIFFUSE: flags = shade_hit<PUPIL_MAT_DIFFUSE>(sc, fp, ps, p, misc); break;
+        case PUPIL_MAT_DIELECTRIC: flags = shade_hit<PUPIL_MAT_DIELECTRIC>(sc, fp, ps, p, misc); break;
+        case PUPIL_MAT_ROUGH_DIELECTRIC: flags = shade_hit<PUPIL_MAT_ROUGH_DIELECTRIC>(sc, fp, ps, p, misc); break;
+        case PUPIL_MAT_CONDUCTOR: flags = shade_hit<PUPIL_MAT_CONDUCTOR>(sc, fp, ps, p, misc); break;
+        case PUPIL_MAT_ROUGH_CONDUCTOR: flags = shade_hit<PUPIL_MAT_ROUGH_CONDUCTOR>(sc, fp, ps, p, misc); break;
+        case PUPIL_MAT_PLASTIC: flags = shade_hit<PUPIL_MAT_PLASTIC>(sc, fp, ps, p, misc); break;
+        case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p, misc); break;
+        default: flags = shade_hit<0u>(sc, fp, ps, p, misc); break;
         }
         if (fp.nee_count) {  // collect_stats only: the reference's shadow-ray count, one atomic per wave
             const unsigned long long m = __ballot((flags & 4u) != 0u);
@@ -1713,12 +1723,22 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, Frame
 }
 
 // ------------------------------------------------------------------ accumulate
-__global__ __launch_bounds__(kShadeBlock) void k_accumulate(FrameParams fp, PathState ps) {
+__global__ __launch_bounds__(kShadeBlock) void k_accumulate(FrameParams fp, PathState ps, const float *aov_src,
+                                                             uint32_t clear_flags) {
     const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= fp.num_local) return;
     const uint32_t out = fp.compact ? l : global_pixel(fp, l);
+    if (aov_src) {  // the frame's AOVs, shaded in an earlier render (pipelined frames)
+        const uint32_t n = fp.num_local;
+        if (fp.albedo)
+            for (int k = 0; k < 3; k++) fp.albedo[3 * out + k] = aov_src[3 * l + k];
+        if (fp.normal)
+            for (int k = 0; k < 3; k++) fp.normal[3 * out + k] = aov_src[3 * n + 3 * l + k];
+        if (fp.test) fp.test[out] = aov_src[6 * n + l];
+    }
     vec3 acc = f3(fp.accum[out]);
     for (uint32_t s = 0; s < fp.spp; s++) {
+        if (clear_flags) ps.sflags[(size_t)s * fp.num_local + l] = 0u;
         vec3 L = f3(ps.rad[(size_t)s * fp.num_local + l]);
         const uint32_t cnt = fp.cnt0 + (fp.accumulate ? s : 0u);
         if (fp.accumulate && cnt > 0) {  // main.cu:187-191
@@ -1952,17 +1972,24 @@ static uint32_t shade_blocks(uint32_t num_paths) {
     return std::max(64u, std::min(1u << 20, (num_paths + kShadeBlock - 1) / kShadeBlock));
 }
 
-void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q,
-                  uint32_t bounce, hipStream_t s, ShadeList list) {
-    const dim3 g(shade_blocks(fp.num_paths)), b(kShadeBlock);
-    if (list == kShadeAll) hipLaunchKernelGGL(k_shade_all<kShadeAll>, g, b, 0, s, sc, fp, ps, q, bounce);
-    else if (list == kShadeNext) hipLaunchKernelGGL(k_shade_all<kShadeNext>, g, b, 0, s, sc, fp, ps, q, bounce);
-    else hipLaunchKernelGGL(k_shade_all<kShadeBins>, g, b, 0, s, sc, fp, ps, q, bounce);
+// max_count: host bound on the paths the launch may list (the device knows the count)
+void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q, uint32_t tag,
+                  hipStream_t s, ShadeList list, uint32_t range_base, uint32_t range_n, uint32_t max_count) {
+    const dim3 g(shade_blocks(max_count)), b(kShadeBlock);
+#define SHADE(L) hipLaunchKernelGGL(k_shade_all<L>, g, b, 0, s, sc, fp, ps, q, tag, range_base, range_n)
+    switch (list) {
+    case kShadeAll: SHADE(kShadeAll); break;
+    case kShadeNext: SHADE(kShadeNext); break;
+    case kShadeNextRange: SHADE(kShadeNextRange); break;
+    default: SHADE(kShadeBins); break;
+    }
+#undef SHADE
 }
 
-void launch_accumulate(const FrameParams &fp, const PathState &ps, hipStream_t s) {
+void launch_accumulate(const FrameParams &fp, const PathState &ps, const float *aov_src, bool clear_flags,
+                       hipStream_t s) {
     const uint32_t blocks = (fp.num_local + kShadeBlock - 1) / kShadeBlock;
-    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kShadeBlock), 0, s, fp, ps);
+    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kShadeBlock), 0, s, fp, ps, aov_src, clear_flags ? 1u : 0u);
 }
 
 }  // namespace pupil

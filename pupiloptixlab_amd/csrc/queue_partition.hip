@@ -103,7 +103,8 @@ constexpr uint32_t kScanChunk = 1024u * kScanPer;
 
 __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nblk, uint32_t nbins,
                                                     uint32_t *counts_out, uint32_t *starts_out,
-                                                    uint32_t *total_out, uint32_t *log_out) {
+                                                    uint32_t *total_out, uint32_t *log_out,
+                                                    unsigned long long *cum_out) {
     __shared__ uint32_t sh[kScanChunk];
     __shared__ uint32_t wave_sum[16];
     __shared__ uint32_t carry_s;
@@ -163,6 +164,7 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nbl
         starts_out[t] = start;
         counts_out[t] = next - start;
         if (log_out) log_out[t] = next - start;
+        if (cum_out) cum_out[t] += next - start;  // one block, stream-ordered: no atomics needed
     }
     if (t == 0 && total_out) *total_out = carry;
 }
@@ -210,7 +212,7 @@ uint32_t partition_hist_entries(uint32_t n) {
 
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
                       uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, uint32_t *log_out,
-                      hipStream_t s) {
+                      hipStream_t s, unsigned long long *cum_out) {
     const uint32_t nblk = part_blocks(n);
     const uint32_t rounds = part_rounds(n);
     if (nblk == 0) {
@@ -224,7 +226,7 @@ void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode 
     hipLaunchKernelGGL(k_part_count<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk,      \
                        rounds);                                                                                    \
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, hist, nblk, nbins, counts_out, starts_out,          \
-                       total_out, log_out);                                                                                 \
+                       total_out, log_out, cum_out);                                                                        \
     hipLaunchKernelGGL(k_part_scatter<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk, out, \
                        rounds)
     switch (mode) {

@@ -33,6 +33,19 @@ struct DistInfo {
 // RANK / WORLD_SIZE / LOCAL_RANK (torchrun's variables); world = 1 without them.
 DistInfo DistFromEnv() noexcept;
 
+// Identity of this launch, the same on every rank of it: the launcher's pid
+// (getppid: torchrun's agent, mpirun, a slurm step), TORCHELASTIC_RUN_ID /
+// _RESTART_COUNT, MASTER_PORT and WORLD_SIZE (PUPIL_RCCL_NONCE overrides it).
+std::string DistLaunchNonce() noexcept;
+// Node-local file through which rank 0 hands its ncclUniqueId to the other ranks:
+// PUPIL_RCCL_ID_FILE, else /tmp/pupil_rccl_<MASTER_PORT>_<hash of the nonce>.id.
+std::string DistIdPath() noexcept;
+// The id file: magic, the launch nonce, the id.  Write removes any previous file first
+// and renames a complete temporary into place.  Read returns 1 (id of this launch),
+// 0 (absent or incomplete) or -1 (left by another launch: never used).
+bool WriteIdFile(const std::string &path, const std::string &nonce, const void *id, size_t size) noexcept;
+int ReadIdFile(const std::string &path, const std::string &nonce, void *id, size_t size) noexcept;
+
 class FrameGather {
 public:
     FrameGather() noexcept = default;

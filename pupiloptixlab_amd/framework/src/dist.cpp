@@ -7,6 +7,8 @@
 #include <cstring>
 #include <thread>
 
+#include <unistd.h>
+
 #include "../../../include/pupil_pt.h"
 #include "pupil/framework.h"
 
@@ -19,23 +21,26 @@ int env_int(const char *name, int def) {
     return v && *v ? std::atoi(v) : def;
 }
 
-// rank 0 -> the others: the 128-byte ncclUniqueId through a file, renamed into place
+constexpr char kIdMagic[8] = {'P', 'U', 'P', 'I', 'L', 'I', 'D', '1'};
+
+// rank 0 -> the others: the 128-byte ncclUniqueId through a file, renamed into place.
+// The file carries the launch nonce (DistLaunchNonce): a file left by an earlier or
+// another launch -- a crashed run, another job on the same MASTER_PORT -- has another
+// nonce and is never used; the other ranks keep waiting for rank 0 to replace it.
 bool exchange_id(const DistInfo &d, const std::string &path, ncclUniqueId &id) {
+    const std::string nonce = DistLaunchNonce();
     if (d.rank == 0) {
         if (ncclGetUniqueId(&id) != ncclSuccess) return false;
-        const std::string tmp = path + ".tmp";
-        FILE *f = std::fopen(tmp.c_str(), "wb");
-        if (!f) return false;
-        const bool ok = std::fwrite(&id, sizeof(id), 1, f) == 1;
-        if (std::fclose(f) != 0 || !ok) return false;
-        return std::rename(tmp.c_str(), path.c_str()) == 0;
+        return WriteIdFile(path, nonce, &id, sizeof(id));
     }
     const auto t0 = std::chrono::steady_clock::now();
+    bool warned = false;
     for (;;) {
-        if (FILE *f = std::fopen(path.c_str(), "rb")) {
-            const bool ok = std::fread(&id, sizeof(id), 1, f) == 1;
-            std::fclose(f);
-            if (ok) return true;
+        const int r = ReadIdFile(path, nonce, &id, sizeof(id));
+        if (r > 0) return true;
+        if (r < 0 && !warned) {
+            Log("rank %d: ignoring %s, left by another launch (waiting for rank 0)", d.rank, path.c_str());
+            warned = true;
         }
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) return false;
         std::this_thread::sleep_for(std::chrono::milliseconds(5));
@@ -48,6 +53,61 @@ __global__ void k_scatter_tiles(const float4 *src, const uint32_t *map, uint32_t
 }
 
 }  // namespace
+
+std::string DistLaunchNonce() noexcept {
+    if (const char *n = std::getenv("PUPIL_RCCL_NONCE"); n && *n) return n;
+    // the ranks of one launch share the launcher process (torchrun's agent, mpirun, a
+    // slurm step) and its run id / restart count / port; another launch differs in one
+    auto env = [](const char *k) {
+        const char *v = std::getenv(k);
+        return std::string(v && *v ? v : "-");
+    };
+    return std::to_string((long long)getppid()) + "." + env("TORCHELASTIC_RUN_ID") + "." +
+           env("TORCHELASTIC_RESTART_COUNT") + "." + env("MASTER_PORT") + "." + env("WORLD_SIZE");
+}
+
+std::string DistIdPath() noexcept {
+    if (const char *p = std::getenv("PUPIL_RCCL_ID_FILE"); p && *p) return p;
+    const char *port = std::getenv("MASTER_PORT");
+    const std::string nonce = DistLaunchNonce();
+    uint64_t h = 1469598103934665603ull;  // FNV-1a of the nonce: one file per launch
+    for (unsigned char c : nonce) h = (h ^ c) * 1099511628211ull;
+    char hex[17];
+    std::snprintf(hex, sizeof(hex), "%016llx", (unsigned long long)h);
+    return "/tmp/pupil_rccl_" + std::string(port && *port ? port : "0") + "_" + hex + ".id";
+}
+
+bool WriteIdFile(const std::string &path, const std::string &nonce, const void *id, size_t size) noexcept {
+    (void)std::remove(path.c_str());  // no reader may see a previous launch's id while this one is written
+    const std::string tmp = path + ".tmp" + std::to_string((long long)getpid());
+    FILE *f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return false;
+    const uint32_t n = (uint32_t)nonce.size();
+    bool ok = std::fwrite(kIdMagic, sizeof(kIdMagic), 1, f) == 1 && std::fwrite(&n, sizeof(n), 1, f) == 1 &&
+              (n == 0 || std::fwrite(nonce.data(), n, 1, f) == 1) && std::fwrite(id, size, 1, f) == 1;
+    ok = std::fclose(f) == 0 && ok;
+    if (!ok) {
+        (void)std::remove(tmp.c_str());
+        return false;
+    }
+    return std::rename(tmp.c_str(), path.c_str()) == 0;
+}
+
+int ReadIdFile(const std::string &path, const std::string &nonce, void *id, size_t size) noexcept {
+    FILE *f = std::fopen(path.c_str(), "rb");
+    if (!f) return 0;
+    char magic[8];
+    uint32_t n = 0;
+    int r = -1;
+    if (std::fread(magic, sizeof(magic), 1, f) == 1 && std::memcmp(magic, kIdMagic, sizeof(magic)) == 0 &&
+        std::fread(&n, sizeof(n), 1, f) == 1 && n == nonce.size()) {
+        std::string got(n, '\0');
+        if ((n == 0 || std::fread(got.data(), n, 1, f) == 1) && got == nonce)
+            r = std::fread(id, size, 1, f) == 1 ? 1 : 0;
+    }
+    std::fclose(f);
+    return r;
+}
 
 DistInfo DistFromEnv() noexcept {
     DistInfo d;
@@ -120,16 +180,17 @@ bool FrameGather::Gather(const void *local, void *full, hipStream_t stream) noex
     if (!m_comm) return false;
     const int world = m_info.world;
     if (ncclGroupStart() != ncclSuccess) return false;
+    bool posted = true;
     if (m_info.rank == 0) {
-        for (int r = 1; r < world; r++)
-            if (ncclRecv(m_staging[(size_t)r], 4 * (size_t)m_counts[(size_t)r], ncclFloat32, r, m_comm, stream) !=
-                ncclSuccess)
-                return false;
-    } else if (ncclSend(local, 4 * (size_t)m_counts[(size_t)m_info.rank], ncclFloat32, 0, m_comm, stream) !=
-               ncclSuccess) {
-        return false;
+        for (int r = 1; r < world && posted; r++)
+            posted = ncclRecv(m_staging[(size_t)r], 4 * (size_t)m_counts[(size_t)r], ncclFloat32, r, m_comm, stream) ==
+                     ncclSuccess;
+    } else {
+        posted = ncclSend(local, 4 * (size_t)m_counts[(size_t)m_info.rank], ncclFloat32, 0, m_comm, stream) ==
+                 ncclSuccess;
     }
-    if (ncclGroupEnd() != ncclSuccess) return false;
+    // the group is closed on every path (an open group would swallow the next RCCL calls)
+    if (ncclGroupEnd() != ncclSuccess || !posted) return false;
     if (m_info.rank != 0) return true;
     for (int r = 0; r < world; r++) {
         const uint32_t n = m_counts[(size_t)r];
@@ -142,3 +203,17 @@ bool FrameGather::Gather(const void *local, void *full, hipStream_t stream) noex
 }
 
 }  // namespace Pupil
+
+// C hooks for the CPU tests of the id-file protocol (tests/test_cpp_host.py)
+extern "C" int pupil_dist_write_id_file(const char *path, const char *nonce, const void *id128) {
+    return Pupil::WriteIdFile(path, nonce, id128, 128) ? 0 : -1;
+}
+extern "C" int pupil_dist_read_id_file(const char *path, const char *nonce, void *id128) {
+    return Pupil::ReadIdFile(path, nonce, id128, 128);
+}
+extern "C" int pupil_dist_id_path(char *out, size_t size) {
+    const std::string p = Pupil::DistIdPath();
+    if (!out || size <= p.size()) return -1;
+    std::memcpy(out, p.c_str(), p.size() + 1);
+    return 0;
+}

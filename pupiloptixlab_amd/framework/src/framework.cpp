@@ -103,11 +103,7 @@ bool System::SetScene(const std::filesystem::path &xml) noexcept {
 bool System::InitDistributed(const DistInfo &d) noexcept {
     device = d.local_rank;
     auto g = std::make_unique<FrameGather>();
-    const char *id = std::getenv("PUPIL_RCCL_ID_FILE");
-    const char *port = std::getenv("MASTER_PORT");
-    const std::string path = id && *id ? std::string(id)
-                                       : "/tmp/pupil_rccl_" + std::string(port && *port ? port : "0") + ".id";
-    if (!g->Init(d, device, path)) return false;
+    if (!g->Init(d, device, DistIdPath())) return false;
     m_gather = std::move(g);
     return true;
 }

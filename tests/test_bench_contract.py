@@ -1,27 +1,63 @@
-"""bench.py's roofline arithmetic (CPU): per-launch normalisation over the timing
-frame's traversal launches, the binding ceiling is the highest fraction, and every
-reported fraction is <= 1 for the r02 config-4 figures."""
+"""bench.py's roofline arithmetic (CPU): per-launch figures from the counter frame's
+per-ray rates times the timed launches' rays per launch, the binding ceiling is the
+highest fraction, and every reported fraction stays <= 1 -- on one GPU and for one
+rank of an 8-way tile shard (whose launches carry 1/8 of the rays: r02 divided the
+whole-frame PMC counts by the rank-local launch time and printed fractions > 1)."""
 import bench
 
 
-def test_roofline_normalises_per_launch_and_picks_the_binding_ceiling(monkeypatch):
-    monkeypatch.setattr(bench, "gather_ceiling", lambda n: {"ceiling_gnodes_per_s": 146.9, "table_mb": 16.8,
-                                                             "per_waves_per_simd": {"7": 145.9}})
-    monkeypatch.setattr(bench, "pmc_record", lambda a: {"traffic_bytes_per_launch": 13.06e9, "round": "r02",
-                                                        "valu_insts_per_launch": 2.78e9, "clock_ghz": 2.23})
+def _patch(monkeypatch):
+    seen = {}
 
-    class A:
-        config = 4
+    def ceiling(footprint):
+        seen["footprint"] = footprint
+        return {"ceiling_gnodes_per_s": 150.0, "table_mb": 67.1, "per_waves_per_simd": {"7": 149.0}}
 
-    # config 4, r02: 1.80 G node visits per frame over 4 traversal launches, 15.6 ms of traversal
-    st = {"node_visits": 1.80e9, "unique_node_fetches": 1.80e9, "trace_bytes": 143.3e9, "bvh_nodes": 267580}
-    r = bench.roofline(A, st, trace_ms=15.64, trace_launches=4)
-    assert abs(r["ms_per_launch"] - 3.91) < 1e-9
+    monkeypatch.setattr(bench, "gather_ceiling", ceiling)
+    # r02 config-4 PMC figures, per traced ray (11.7 GB and 2.63 G VALU per 26.6 M-ray launch)
+    monkeypatch.setattr(bench, "pmc_record", lambda a: {"traffic_bytes_per_ray": 440.4, "round": "r03",
+                                                        "valu_insts_per_ray": 98.7, "clock_ghz": 2.20})
+    return seen
+
+
+class A:
+    config = 4
+
+
+# counter frame: 98.4 M rays, 1.80 G node visits, 143.3 GB algorithmic
+ST = {"primary_rays": 16588800, "extension_rays": 48300000, "shadow_rays": 33511200, "node_visits": 1.80e9,
+      "unique_node_fetches": 0.92e9, "trace_bytes": 143.3e9, "bvh_nodes": 212619, "bvh_prims": 1000014}
+
+
+def test_roofline_one_gpu_per_launch_and_binding_ceiling(monkeypatch):
+    seen = _patch(monkeypatch)
+    # 5 timed steps, one pipelined launch each carrying one frame's rays, 14.0 ms each
+    timed = {"trace_ms": 70.0, "launches": 5, "rays": 5 * 98.4e6}
+    r = bench.roofline(A, ST, timed)
+    assert abs(r["ms_per_launch"] - 14.0) < 1e-9 and r["launches"] == 5
+    assert abs(r["rays_per_launch"] - 98.4e6) < 1
     c = r["ceilings"]
-    assert abs(c["node-gather"]["achieved"] - 1.80e9 / 4 / 3.91e-3 / 1e9) < 0.01
+    rays_cf = ST["primary_rays"] + ST["extension_rays"] + ST["shadow_rays"]
+    f = 98.4e6 / rays_cf
+    assert abs(c["node-gather"]["achieved"] - 0.92e9 * f / 14.0e-3 / 1e9) < 0.01
+    assert abs(c["valu-issue"]["frac"] - 2 * 98.7 * 98.4e6 / (1024 * 2.20e9 * 14.0e-3)) < 1e-3
+    assert abs(c["hbm"]["frac"] - 440.4 * 98.4e6 / 14.0e-3 / 8e12) < 1e-3
+    assert abs(r["traffic"] - 440.4 * 98.4e6) < 1e3
+    assert abs(r["algorithmic"]["bytes_per_launch"] - 143.3e9 * f) < 1e3
     assert all(0 < v["frac"] <= 1 for v in c.values())
-    assert r["bound"] == max(c, key=lambda k: c[k]["frac"]) == "node-gather"
-    assert r["frac"] == c["node-gather"]["frac"]
-    assert abs(c["valu-issue"]["frac"] - 2 * 2.78e9 / (1024 * 2.23e9 * 3.91e-3)) < 1e-3
-    assert abs(c["hbm"]["frac"] - 13.06e9 / 3.91e-3 / 8e12) < 1e-3
+    assert r["bound"] == max(c, key=lambda k: c[k]["frac"])
+    assert r["frac"] == c[r["bound"]]["frac"]
     assert list(r)[:6] == ["bound", "achieved", "peak", "unit", "frac", "traffic"]
+    # the gather ceiling is measured on a table no smaller than nodes + records
+    assert seen["footprint"] == 64.0 * 212619 + 48.0 * 1000014
+
+
+def test_roofline_rank_of_an_8_way_shard_stays_below_one(monkeypatch):
+    _patch(monkeypatch)
+    # one rank of 8: 1/8 of the rays per launch, launches longer than 1/8 (the launch tail)
+    one = bench.roofline(A, ST, {"trace_ms": 70.0, "launches": 5, "rays": 5 * 98.4e6})
+    rank = bench.roofline(A, ST, {"trace_ms": 5 * 2.2, "launches": 5, "rays": 5 * 98.4e6 / 8})
+    for k, v in rank["ceilings"].items():
+        assert 0 < v["frac"] <= 1, (k, v["frac"])
+        assert v["frac"] < one["ceilings"][k]["frac"]  # the same work per ray, less of it per second
+    assert abs(rank["traffic"] - one["traffic"] / 8) < 1e3

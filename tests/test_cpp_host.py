@@ -144,3 +144,40 @@ def test_framework_links_rccl():
     assert "librccl" in out
     syms = subprocess.run(["nm", "-DC", FW], capture_output=True, text=True, check=True).stdout
     assert "Pupil::FrameGather::Gather(void const*, void*, ihipStream_t*)" in syms
+
+
+def test_rccl_id_file_rejects_a_stale_launch(tmp_path, monkeypatch):
+    """The C++ drop-in's RCCL id hand-over (framework/src/dist.cpp): a file left by another
+    launch (a crashed run, another job on the same MASTER_PORT) carries another launch
+    nonce and is never read as this launch's id; rank 0's write replaces it atomically;
+    an incomplete file reads as absent; the default path is per launch."""
+    _built()
+    import ctypes as C
+
+    lib = C.CDLL(FW)
+    lib.pupil_dist_write_id_file.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p]
+    lib.pupil_dist_read_id_file.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p]
+    lib.pupil_dist_id_path.argtypes = [C.c_char_p, C.c_size_t]
+    path = str(tmp_path / "pupil_rccl.id").encode()
+    old, new = bytes(range(128)), bytes(reversed(range(128)))
+    buf = C.create_string_buffer(128)
+    assert lib.pupil_dist_read_id_file(path, b"launch-2", buf) == 0  # absent
+    assert lib.pupil_dist_write_id_file(path, b"launch-1", old) == 0  # a crashed earlier launch
+    assert lib.pupil_dist_read_id_file(path, b"launch-2", buf) == -1  # stale: rejected
+    assert lib.pupil_dist_read_id_file(path, b"launch-1", buf) == 1 and buf.raw == old
+    assert lib.pupil_dist_write_id_file(path, b"launch-2", new) == 0  # rank 0 of the new launch
+    assert lib.pupil_dist_read_id_file(path, b"launch-2", buf) == 1 and buf.raw == new
+    with open(path, "rb") as f:
+        whole = f.read()
+    with open(path, "wb") as f:  # torn file: nonce present, id cut short
+        f.write(whole[:-10])
+    assert lib.pupil_dist_read_id_file(path, b"launch-2", buf) == 0
+    out = C.create_string_buffer(512)
+    monkeypatch.delenv("PUPIL_RCCL_ID_FILE", raising=False)
+    monkeypatch.setenv("MASTER_PORT", "29511")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "a")
+    assert lib.pupil_dist_id_path(out, 512) == 0
+    pa = out.value
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "b")
+    assert lib.pupil_dist_id_path(out, 512) == 0
+    assert pa.startswith(b"/tmp/pupil_rccl_29511_") and out.value != pa

@@ -60,6 +60,7 @@ def check_sample(desc, spp, stride, name, offset=0):
     assert exact == len(pixels)
     assert np.array_equal(gpu["albedo"].reshape(n, 3)[pixels], ref["albedo"])
     assert np.array_equal(gpu["normal"].reshape(n, 3)[pixels], ref["normal"])
+    return st
 
 
 def test_config2_materials_1024_64spp():
@@ -81,7 +82,15 @@ def test_config4_field_1m():
     check_sample(desc, 8, 1, "config4")
 
 
-def test_config5_instanced_10m():
-    """40 instances x 250k-triangle BLAS (10M triangles), 3840x2160, 16 spp, depth 6."""
+@pytest.mark.parametrize("accel", ["two_level", "flat"])
+def test_config5_instanced_10m(accel, monkeypatch):
+    """40 instances x 250k-triangle BLAS (10M triangles), 3840x2160, 16 spp, depth 6, on
+    the two-level structure BASELINE names (world-mode BLAS copies, braided TLAS whose
+    large entry ranges are split by the binned SAH -- the structure bench.py --config 5
+    times) and on the flattened BVH."""
+    monkeypatch.setenv("PUPIL_ACCEL", accel)
     desc = scenes.instanced_field(40, 3840, 2160, 6, seed=2, spheres_per_blas=125).desc()
-    check_sample(desc, 16, 97, "config5", offset=11)
+    st = check_sample(desc, 16, 97, f"config5-{accel}", offset=11)
+    assert st["two_level"] == (accel == "two_level")
+    if accel == "two_level":  # ~40 x 1024 braided TLAS entries: the binned-SAH split ran
+        assert st["tlas_sah_splits"] > 0, st["tlas_sah_splits"]

@@ -505,13 +505,20 @@ def test_camera_change_uploads_new_sensor():
     assert np.array_equal(moved.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("case", ["flat", "two_level", "bins", "batched", "hint"])
-def test_render_ahead_onrun_sequence(case, monkeypatch):
-    """Render-ahead (engine.hip, PUPIL_AHEAD): the last mixed launch of an OnRun traces
-    the camera rays of the next OnRun.  A sequence of OnRuns on one engine must equal
-    the oracle after every frame, including when the camera moves (the traced-ahead
-    rays belong to the old view), when the seed jumps (they belong to another frame),
-    after an instance update, and for max_depth 1 (no mixed launch to ride in)."""
+PIPE_CASES = ["flat", "two_level", "two_level_world", "bins", "batched", "hint", "deep", "pipe3", "tiles"]
+
+
+@pytest.mark.parametrize("case", PIPE_CASES)
+def test_pipelined_onrun_sequence(case, monkeypatch):
+    """Pipelined frames (engine.hip render_pipelined): consecutive renders that continue
+    each other keep up to max_depth frames in flight, and each render's launches advance
+    all of them.  A sequence of OnRuns on one engine must equal the oracle after every
+    render -- accumulation, "final result" and the AOVs (albedo / normal / test of the
+    render's own frame, shaded renders earlier and kept in the slot scratch) -- including
+    when the camera moves, an instance moves, the seed jumps or max_depth changes (the
+    frames in flight are dropped), on multi-material scenes (material partition over the
+    ring), two-level structures, batched renders (PUPIL_AHEAD=2 / the hint), a ring
+    capped below max_depth (PUPIL_PIPE=3) and tile-sharded compact buffers."""
     import torch
     from pupiloptixlab_amd.pt_pass import PTPass, Events
     from pupiloptixlab_amd import world as W
@@ -519,51 +526,124 @@ def test_render_ahead_onrun_sequence(case, monkeypatch):
     if case == "two_level":
         monkeypatch.setenv("PUPIL_ACCEL", "two_level")
         monkeypatch.setenv("PUPIL_TL_MODE", "object")
+    if case == "two_level_world":
+        monkeypatch.setenv("PUPIL_ACCEL", "two_level")
     if case == "batched":
         monkeypatch.setenv("PUPIL_AHEAD", "2")
+    if case == "pipe3":
+        monkeypatch.setenv("PUPIL_PIPE", "3")
     if case == "bins":
         w = World().load_scene(scenes.cornell_materials_xml(os.path.join(TMP, "cbmat48.xml"), 48, 40, 5))
-    elif case == "two_level":
+    elif case in ("two_level", "two_level_world"):
         w = scenes.instanced_field(num_instances=6, width=48, height=32, max_depth=5, seed=2, spheres_per_blas=8)
-    elif case == "flat":
+    elif case in ("flat", "tiles"):
         w = scenes.sphere_field(8, 48, 32, 4, seed=5, merge=False)
+    elif case in ("deep", "pipe3"):
+        w = World().load_scene(scenes.cornell_xml(os.path.join(TMP, "cb40d8.xml"), 40, 40, 8))
     else:
         w = _cornell(48)
     spp = 2 if case in ("batched", "hint") else 1  # hint: PUPIL_HINT_CONTINUE on batched renders
     pt = PTPass(device=0)
     pt.set_scene(w)
+    if case == "tiles":
+        pt.set_tiling(16, 1, 3)
+    depth = w.desc().max_depth
+    slots = min(depth, 3) if case == "pipe3" else depth
+    keys = ("pt accum buffer", "final result", "albedo", "normal", "test")
 
-    def step(k_frames, o, seed0=0, depth=0):
+    def step(k_frames, o, seed0=0, max_depth=0):
         pt.render(spp, continues=case == "hint")
         torch.cuda.synchronize()
-        got = pt.buffers.get("pt accum buffer").cpu().numpy()
-        ref = o.render(spp=k_frames * spp, random_seed=seed0, max_depth=depth)["accum"]
-        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (case, k_frames, seed0)
+        got = {k: pt.buffers.get(k).cpu().numpy() for k in keys}
+        px = pt.local_pixels() if case == "tiles" else None
+        ref = o.render(spp=k_frames * spp, random_seed=seed0, max_depth=max_depth, pixels=px)
+        for k, rk in zip(keys, ("accum", "accum", "albedo", "normal", "test")):
+            assert np.array_equal(got[k].reshape(ref[rk].shape).view(np.uint32), ref[rk].view(np.uint32)), \
+                (case, k, k_frames, seed0)
 
     o = oracle.OracleScene(w.desc())
-    for k in range(1, 4):
+    for k in range(1, 2 * slots + 2):  # long enough to reach one launch per render
         step(k, o)
-    if case in ("flat", "batched", "hint"):  # the camera moves: accumulation restarts on the new view
+    st = pt.stats()
+    assert st["pipeline_slots"] == slots and st["frames_in_flight"] == slots - 1, (case, st["pipeline_slots"],
+                                                                                  st["frames_in_flight"])
+    if case in ("flat", "batched", "hint", "tiles"):  # the camera moves: accumulation restarts on the new view
         w.set_sensor(40.0, W.look_at_mitsuba((0.3, 1.2, 3.5), (0.0, 0.9, 0.0), (0.0, 1.0, 0.0)), fov_axis="x")
         pt.events.dispatch(Events.CAMERA_CHANGE)
         o = oracle.OracleScene(w.desc())
-        for k in range(1, 3):
+        for k in range(1, slots + 2):
             step(k, o)
-    if case in ("flat", "two_level"):  # an instance moves: the rays traced ahead hit the old geometry
+    if case in ("flat", "two_level", "two_level_world"):  # an instance moves: frames in flight hit the old geometry
         w.set_instance_transform(1, W.transform(scale=(1.5, 1.5, 1.5), rotate=((0, 1, 0), 30), translate=(0.5, 1.0, -0.5)))
         pt.update_instance(w, 1)
         o = oracle.OracleScene(w.desc())
-        for k in range(1, 3):
+        for k in range(1, slots + 2):
             step(k, o)
-    # the seed jumps: the rays traced ahead for the next seed are not used
+    # the seed jumps: the frames started for the next seeds are not used
     pt.random_seed, pt.sample_cnt = 9, 0
     step(1, o, seed0=9)
-    # max_depth 1: no mixed launch, so no render-ahead; the next render still matches
+    step(2, o, seed0=9)
+    # max_depth changes (the inspector): frames in flight were shaded for the old depth
+    pt.max_depth = 2
+    pt.random_seed, pt.sample_cnt = 0, 0
+    for k in range(1, 4):
+        step(k, o, max_depth=2)
+    # max_depth 1: a frame is one launch, nothing to pipeline; the next render still matches
     pt.max_depth = 1
     pt.random_seed, pt.sample_cnt = 0, 0
-    step(1, o, depth=1)
-    step(2, o, depth=1)
+    step(1, o, max_depth=1)
+    step(2, o, max_depth=1)
     pt.close_engine()
+
+
+def test_pipelined_ray_accounting():
+    """rays_traced_total (device running totals of the flags partitions + the host's camera
+    rays) equals the sum of the per-render ray counts over a pipelined OnRun sequence, and,
+    with pipelining off (PUPIL_PIPE=1), the oracle's ray counts frame by frame."""
+    import torch
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    w = _cornell(48, depth=5)
+    o = oracle.OracleScene(w.desc())
+    totals = {}
+    for pipe in ("0", "1"):
+        os.environ["PUPIL_PIPE"] = pipe
+        try:
+            pt = PTPass(device=0)
+            pt.set_scene(w)
+        finally:
+            del os.environ["PUPIL_PIPE"]
+        t0 = pt.stats()["rays_traced_total"]
+        per = 0
+        for _ in range(12):
+            pt.render(1)
+            torch.cuda.synchronize()
+            c = pt.stats()
+            per += c["primary_rays"] + c["extension_rays"] + c["shadow_rays"]
+        t1 = pt.stats()["rays_traced_total"]
+        assert t1 - t0 == per, (pipe, t1 - t0, per)
+        totals[pipe] = (per, pt.stats()["frames_in_flight"])
+        pt.close_engine()
+    rs = o.render(spp=12)["stats"]
+    assert totals["1"] == (rs["primary_rays"] + rs["extension_rays"] + rs["shadow_rays"], 0)
+    # pipelined: the 12 completed frames plus part of the 4 frames in flight
+    assert totals["0"][1] == 4 and totals["0"][0] > totals["1"][0]
+
+
+def test_max_depth_above_128_renders():
+    """The reference takes integrator.max_depth unclamped at SetScene (pt_pass.cpp:112-115;
+    only the inspector clamps to 1..128): a scene with max_depth 150 renders exactly like
+    the oracle (per-bounce flags tags alias above 63 bounces, so the flags are cleared per
+    bounce, and the ray log grows with the depth)."""
+    w = World().load_scene(scenes.cornell_xml(os.path.join(TMP, "cb24d150.xml"), 24, 24, 150))
+    desc = w.desc()
+    assert desc.max_depth == 150
+    gpu = render_gpu(desc, 2)
+    ref = oracle.OracleScene(desc).render(spp=2)
+    assert np.array_equal(gpu["pt accum buffer"].view(np.uint32), ref["accum"].view(np.uint32))
+    s, rs = gpu["stats"], ref["stats"]
+    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
+        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
 
 
 def test_render_orders_with_torch_default_stream():
@@ -630,24 +710,6 @@ def test_skewed_scene_stays_within_stack_capacity(accel, monkeypatch):
         out = _trace(desc, rays)
         bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
         assert not bad.any(), f"{accel} bvh{width} refill {refill}: {bad.sum()} rays differ"
-
-
-def test_render_rejects_max_depth_above_128():
-    """The C ABI refuses max_depth > 128 (PTPass's inspector range, pt_pass.cpp:225-237)
-    instead of silently under-counting rays past the per-bounce log."""
-    import ctypes as C
-    from pupiloptixlab_amd.pt_pass import PTPass
-
-    pt = PTPass(device=0)
-    pt.set_scene(_cornell(16).desc())
-    la = abi.Launch()
-    la.spp, la.max_depth, la.accumulate, la.tile_size, la.tile_world = 1, 129, 1, 32, 1
-    f = pt._frame()
-    assert pt._lib.pupil_pt_render(pt._pt, C.byref(f), C.byref(la), None) == abi.ERR_INVALID
-    la.max_depth = 128
-    assert pt._lib.pupil_pt_render(pt._pt, C.byref(f), C.byref(la), None) == 0
-    pt.stats()
-    pt.close_engine()
 
 
 def _emissive_field(spheres=24, w=96, h=64, groups=2):

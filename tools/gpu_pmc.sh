@@ -7,7 +7,7 @@ mkdir -p gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 CFG=${CONFIG:-4}
-ARGS="--steps 2 --warmup 1 --cpu-baseline 0 --config $CFG ${BENCH_ARGS:-}"
+ARGS="--steps 3 --warmup 4 --cpu-baseline 0 --dropin 0 --config $CFG ${BENCH_ARGS:-}"
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM SQ_INSTS_LDS" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" "SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE" ${EXTRA_SETS:-}; do
   i=$((i+1))
@@ -16,7 +16,7 @@ for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INS
   [ "$rc" -eq 0 ] || exit $rc
 done
 cd $R
-K=${PMC_KERNELS:-"k_trace4<0, false, false>|k_trace4<3, false, false>"}
-PUPIL_ROUND=${PUPIL_ROUND:-r02} python3 tools/pmc_summary.py gpurun_out/pmc --json "$K" gpurun_out/pmc_config$CFG.json \
-  "config $CFG default bench: all non-instrumented k_trace4 launches (primary extend + per-bounce mixed extension/shadow)"
+K=${PMC_KERNELS:-"k_trace4<0, false, false>|k_trace4<3, false, false>|k_trace4<4, false, false>"}
+PUPIL_ROUND=${PUPIL_ROUND:-r03} python3 tools/pmc_summary.py gpurun_out/pmc --json "$K" gpurun_out/pmc_config$CFG.json \
+  "config $CFG default bench: all non-instrumented k_trace4 launches (primary extend, mixed extension/shadow, pipelined mixed + camera rays)"
 python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt

@@ -57,6 +57,20 @@ def traffic_json(root, kernels, out_path, note=""):
         v = [x for k in ks for x in vals[k].get(c, [])]
         return sum(v) / max(1, len(v))
 
+    def total(c):
+        return sum(x for k in ks for x in vals[k].get(c, []))
+
+    # rays the plain traversal kernels traced in each pass (bench.py's JSON line,
+    # config.rays_traced_plain_process): identical work in every pass
+    rays = set()
+    for lg in sorted(glob.glob(os.path.join(root, "p*.log"))):
+        for line in open(lg):
+            if line.startswith("{") and '"metric"' in line:
+                rays.add(json.loads(line)["config"].get("rays_traced_plain_process"))
+    rays.discard(None)
+    assert len(rays) <= 1, f"passes traced different ray counts: {rays}"
+    n_rays = rays.pop() if rays else None
+
     f, w = pooled("FETCH_SIZE"), pooled("WRITE_SIZE")
     hit, miss = pooled("TCC_HIT_sum"), pooled("TCC_MISS_sum")
     d = [x for k in ks for x in dur[k]]
@@ -71,6 +85,12 @@ def traffic_json(root, kernels, out_path, note=""):
            # 8 XCDs, so the engine clock is GRBM / 8 / launch time
            "valu_insts_per_launch": valu or None,
            "clock_ghz": (grbm / 8.0 / (avg_ms * 1e-3) / 1e9) if grbm else None,
+           # per traced ray over all dispatches of the pass (launch sizes vary: pipelined
+           # launches, a rank's tiles), what bench.py scales by its own rays per launch
+           "rays_traced": n_rays,
+           "traffic_bytes_per_ray": (2.0 * total("FETCH_SIZE") + total("WRITE_SIZE")) * 1024.0 / n_rays if n_rays else None,
+           "valu_insts_per_ray": total("SQ_INSTS_VALU") / n_rays if n_rays and valu else None,
+           "dispatches": len(d),
            "note": note}
     with open(out_path, "w") as fh:
         json.dump(rec, fh, indent=1)
