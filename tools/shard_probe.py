@@ -23,8 +23,12 @@ def main():
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--progressive", type=int, default=0,
                     help="1: every frame continues the previous one (seeds 8k..8k+7, accumulating) with "
-                         "PUPIL_HINT_CONTINUE, so each frame's camera rays ride in the previous frame's last "
-                         "launch (render-ahead); 0: every frame re-renders seed 0 like bench.py")
+                         "PUPIL_HINT_CONTINUE, so frames are pipelined (one traversal launch per frame in the "
+                         "steady state), as bench.py renders; 0: every frame re-renders seed 0")
+    ap.add_argument("--warmup", type=int, default=4, help="untimed frames per rank (fill the frame pipeline)")
+    ap.add_argument("--onrun", type=int, default=0,
+                    help="1: the drop-in cadence -- a frame is 8 renders of 1 spp, each followed by a device "
+                         "synchronisation (PTPass::OnRun, pt_pass.cpp:51-56), continuing one progressive render")
     args = ap.parse_args()
     import torch
 
@@ -42,15 +46,25 @@ def main():
         for r in range(n):
             pt.set_tiling(args.tile, r, n)
             pt.mark_dirty()
-            pt.render(8, stream=s, continues=bool(args.progressive))
+
+            def frame():
+                if args.onrun:
+                    for _ in range(8):
+                        pt.render(1, stream=s)
+                        s.synchronize()
+                else:
+                    if not args.progressive:
+                        pt.mark_dirty()
+                    pt.render(8, stream=s, continues=bool(args.progressive))
+
+            for _ in range(max(1, args.warmup)):
+                frame()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             host = 0.0
             for _ in range(args.frames):
-                if not args.progressive:
-                    pt.mark_dirty()
                 h0 = time.perf_counter()
-                pt.render(8, stream=s, continues=bool(args.progressive))
+                frame()
                 host += time.perf_counter() - h0
             torch.cuda.synchronize()
             per_rank.append((time.perf_counter() - t0) / args.frames * 1e3)
