@@ -1156,14 +1156,14 @@ struct Node {
 
 // The engine's quantized BVH4 node (pupiloptixlab_amd/csrc/pt_scene.h Bvh4Node,
 // 64 B), for CPU traversal of the GPU's own arrays (oracle_set_bvh4): child k's
-// plane on an axis is o + q_k * 2^(e-127); link >= 0 inner node, < 0 leaf with
-// ~link = first_record << 3 | (count - 1), kQEmpty unused.
+// plane on an axis is o + q_k * s (s a power of two, one float per axis); link >= 0
+// inner node, < 0 leaf with ~link = first_record << 3 | (count - 1), kQEmpty unused.
 struct QNode {
     float ox, oy, oz;
-    uint32_t exps;
+    float sx;
     int32_t child[4];
     uint32_t qlo[3], qhi[3];
-    uint32_t pad[2];
+    float sy, sz;
 };
 static_assert(sizeof(QNode) == 64, "Bvh4Node layout");
 constexpr int32_t kQEmpty = 0x7FFFFFFF, kQDone = 0x76543210;
@@ -1280,9 +1280,7 @@ struct Scene {
         float bn[3], an[3], af[3];
         uint32_t qn[3], qf[3];
         for (int a = 0; a < 3; a++) {
-            uint32_t sb = ((n.exps >> (8 * a)) & 0xFFu) << 23;
-            float sc;
-            std::memcpy(&sc, &sb, 4);
+            const float sc = a == 0 ? n.sx : (a == 1 ? n.sy : n.sz);
             const float A = o[a] - ro[a];
             const float av = A * id[a];
             const float e = std::fma(512.f, sc, std::fabs(A) + std::fabs(o[a])) * (std::fabs(id[a]) * 0x1p-21f);

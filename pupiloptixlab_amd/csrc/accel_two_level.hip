@@ -394,8 +394,7 @@ bool world_entries(TwoLevelAccel &acc, const DevInstance &d, uint32_t id, uint32
                 continue;
             }
             const Bvh4Node &n = top[(size_t)j];
-            const float sc3[3] = {qfloat((n.exps & 0xFFu) << 23), qfloat(((n.exps >> 8) & 0xFFu) << 23),
-                                  qfloat(((n.exps >> 16) & 0xFFu) << 23)};
+            const float sc3[3] = {n.sx, n.sy, n.sz};
             const float org[3] = {n.ox, n.oy, n.oz};
             const uint32_t qlo[3] = {n.qlo_x, n.qlo_y, n.qlo_z}, qhi[3] = {n.qhi_x, n.qhi_y, n.qhi_z};
             for (int k = 0; k < 4; k++) {
@@ -709,6 +708,9 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         return -1;
     }
     acc.num_wprims = (uint32_t)wbase;
+    // the traversal addresses nodes by 32-bit offsets (kMaxNodes4): instance copies beyond
+    // that take the object-space structure, whose BLASes are shared
+    if (acc.world && wnodes > kMaxNodes4) acc.world = false;
     if (acc.world) {  // world BLAS copies + sphere records appended to the world records
         acc.entries.assign(n, {});
         acc.inst_shape = shape_of;

@@ -79,6 +79,13 @@ PT_HD void quantize_axis(float lo, float hi, const float *clo, const float *chi,
     quantize_axis_n<4>(lo, hi, clo, chi, nk, origin, ebyte, &qlo, &qhi);
 }
 
+// The per-axis plane scales of a node from their biased exponents.
+PT_HD void set_scales(Bvh4Node &o, uint32_t ex, uint32_t ey, uint32_t ez) {
+    o.sx = qfloat(ex << 23);
+    o.sy = qfloat(ey << 23);
+    o.sz = qfloat(ez << 23);
+}
+
 // One BVH4 node from its box, nk <= 4 child boxes and links.
 PT_HD Bvh4Node encode_bvh4(const float nlo[3], const float nhi[3], const float clo[3][4], const float chi[3][4],
                            const int link[4], int nk) {
@@ -87,9 +94,8 @@ PT_HD Bvh4Node encode_bvh4(const float nlo[3], const float nhi[3], const float c
     quantize_axis(nlo[0], nhi[0], clo[0], chi[0], nk, o.ox, ex, o.qlo_x, o.qhi_x);
     quantize_axis(nlo[1], nhi[1], clo[1], chi[1], nk, o.oy, ey, o.qlo_y, o.qhi_y);
     quantize_axis(nlo[2], nhi[2], clo[2], chi[2], nk, o.oz, ez, o.qlo_z, o.qhi_z);
-    o.exps = ex | (ey << 8) | (ez << 16);
+    set_scales(o, ex, ey, ez);
     for (int k = 0; k < 4; k++) o.child[k] = k < nk ? link[k] : kEmptyLink;
-    o.pad[0] = o.pad[1] = 0u;
     return o;
 }
 

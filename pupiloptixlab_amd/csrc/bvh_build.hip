@@ -601,9 +601,8 @@ __global__ void k_emit4(int n, const uint32_t *sorted_vals, const Aabb *prim_box
     quantize_axis(nb.lo[0], nb.hi[0], clo[0], chi[0], nk, o.ox, ex, o.qlo_x, o.qhi_x);
     quantize_axis(nb.lo[1], nb.hi[1], clo[1], chi[1], nk, o.oy, ey, o.qlo_y, o.qhi_y);
     quantize_axis(nb.lo[2], nb.hi[2], clo[2], chi[2], nk, o.oz, ez, o.qlo_z, o.qhi_z);
-    o.exps = ex | (ey << 8) | (ez << 16);
+    set_scales(o, ex, ey, ez);
     for (int k = 0; k < 4; k++) o.child[k] = k < nk ? link[k] : kEmptyLink;
-    o.pad[0] = o.pad[1] = 0u;
     nodes4[idx4[i]] = o;
 }
 
@@ -699,9 +698,8 @@ __global__ void k_collapse_emit(int items, int base, int next_base, const int *i
     quantize_axis(nb.lo[0], nb.hi[0], clo[0], chi[0], nk, o.ox, ex, o.qlo_x, o.qhi_x);
     quantize_axis(nb.lo[1], nb.hi[1], clo[1], chi[1], nk, o.oy, ey, o.qlo_y, o.qhi_y);
     quantize_axis(nb.lo[2], nb.hi[2], clo[2], chi[2], nk, o.oz, ez, o.qlo_z, o.qhi_z);
-    o.exps = ex | (ey << 8) | (ez << 16);
+    set_scales(o, ex, ey, ez);
     for (int k = 0; k < 4; k++) o.child[k] = k < nk ? link[k] : kEmptyLink;
-    o.pad[0] = o.pad[1] = 0u;
     nodes4[base + t] = o;
 }
 

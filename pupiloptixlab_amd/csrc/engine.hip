@@ -379,6 +379,11 @@ int ensure_state(pupil_pt *pt, size_t paths) {
 
 // Local pixel list of a rank: tiles t with t % world == rank, row-major tile
 // order, row-major pixels inside a tile (clipped at the image border).
+// BVH4 node array the traversal walks (its size bounds the 32-bit node offsets, kMaxNodes4)
+uint64_t nodes4_count(const pupil_pt *pt) {
+    return pt->two_level ? (pt->tl.world ? pt->tl.num_wnodes : pt->tl.num_nodes4) : pt->bvh.num_nodes4;
+}
+
 uint32_t local_pixels(uint32_t w, uint32_t h, uint32_t ts, uint32_t rank, uint32_t world, uint32_t *out) {
     if (world <= 1) {
         if (out)
@@ -893,6 +898,8 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
+    if (sc.bvh_width == 4 && nodes4_count(pt) > kMaxNodes4)
+        return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "BVH4 larger than 2^26 nodes (32-bit node offsets)"));
     sc.prim_inst = d_prim_inst;
     sc.instances = d_insts;
     sc.materials = d_mats;

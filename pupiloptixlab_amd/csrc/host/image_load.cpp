@@ -136,6 +136,17 @@ bool exr_rle(const uint8_t *p, size_t n, std::vector<uint8_t> &out, size_t expec
     return out.size() == expect;
 }
 
+// NUL-terminated string at f[at] that must end before `limit` (untrusted input: no
+// read past the buffer when the terminator is missing)
+bool read_cstr(const std::vector<uint8_t> &f, size_t at, size_t limit, std::string &out) {
+    limit = std::min(limit, f.size());
+    if (at >= limit) return false;
+    const void *z = std::memchr(f.data() + at, 0, limit - at);
+    if (!z) return false;
+    out.assign(reinterpret_cast<const char *>(f.data() + at), static_cast<const uint8_t *>(z) - (f.data() + at));
+    return true;
+}
+
 bool load_exr(const std::vector<uint8_t> &f, std::vector<float> &rgba, int &w, int &h, std::string &err) {
     size_t pos = 0;
     auto need = [&](size_t k) { return pos + k <= f.size(); };
@@ -159,10 +170,10 @@ bool load_exr(const std::vector<uint8_t> &f, std::vector<float> &rgba, int &w, i
             pos++;
             break;
         }
-        const std::string name(reinterpret_cast<const char *>(f.data() + pos));
+        std::string name, type;
+        if (!read_cstr(f, pos, f.size(), name)) return err = "truncated EXR header", false;
         pos += name.size() + 1;
-        if (!need(1)) return err = "truncated EXR header", false;
-        const std::string type(reinterpret_cast<const char *>(f.data() + pos));
+        if (!read_cstr(f, pos, f.size(), type)) return err = "truncated EXR header", false;
         pos += type.size() + 1;
         if (!need(4)) return err = "truncated EXR header", false;
         const int32_t size = rd32(pos);
@@ -173,7 +184,7 @@ bool load_exr(const std::vector<uint8_t> &f, std::vector<float> &rgba, int &w, i
             size_t q = pos;
             while (q < end && f[q] != 0) {
                 ExrChannel c;
-                c.name = std::string(reinterpret_cast<const char *>(f.data() + q));
+                if (!read_cstr(f, q, end, c.name)) return err = "bad EXR channel list", false;
                 q += c.name.size() + 1;
                 if (q + 16 > end) return err = "bad EXR channel list", false;
                 c.type = rd32(q);
@@ -194,9 +205,10 @@ bool load_exr(const std::vector<uint8_t> &f, std::vector<float> &rgba, int &w, i
     }
     (void)line_order;  // chunks carry their own first line number
     if (!have_dw || ch.empty() || comp < 0) return err = "EXR header lacks channels / compression / dataWindow", false;
-    w = dw[2] - dw[0] + 1;
-    h = dw[3] - dw[1] + 1;
-    if (w <= 0 || h <= 0 || (int64_t)w * h > (1ll << 28)) return err = "bad EXR data window", false;
+    const int64_t w64 = (int64_t)dw[2] - dw[0] + 1, h64 = (int64_t)dw[3] - dw[1] + 1;
+    if (w64 <= 0 || h64 <= 0 || w64 * h64 > (1ll << 28)) return err = "bad EXR data window", false;
+    w = (int)w64;
+    h = (int)h64;
     for (const auto &c : ch)
         if (c.xs != 1 || c.ys != 1 || c.type < 0 || c.type > 2) return err = "EXR channel sampling / type not supported", false;
     int lines;
@@ -214,12 +226,14 @@ bool load_exr(const std::vector<uint8_t> &f, std::vector<float> &rgba, int &w, i
     for (int k = 0; k < chunks; k++) {
         uint64_t off;
         std::memcpy(&off, f.data() + pos + 8 * (size_t)k, 8);
-        if (off + 8 > f.size()) return err = "bad EXR chunk offset", false;
+        // offsets come from the file: compare without forming off + k (no wrap-around)
+        if (off > f.size() || f.size() - off < 8) return err = "bad EXR chunk offset", false;
         const int32_t y0 = rd32((size_t)off), size = rd32((size_t)off + 4);
+        if (size < 0 || (uint64_t)size > f.size() - off - 8) return err = "truncated EXR chunk", false;
         const uint8_t *src = f.data() + off + 8;
-        if (size < 0 || off + 8 + (uint64_t)size > f.size()) return err = "truncated EXR chunk", false;
-        const int first = y0 - dw[1];
-        if (first < 0 || first >= h) return err = "EXR chunk outside the data window", false;
+        const int64_t first64 = (int64_t)y0 - dw[1];
+        if (first64 < 0 || first64 >= h) return err = "EXR chunk outside the data window", false;
+        const int first = (int)first64;
         const int nl = std::min(lines, h - first);
         const size_t expect = bpl * (size_t)nl;
         if ((size_t)size == expect || comp == 0) {  // stored uncompressed
@@ -837,6 +851,11 @@ struct Jpeg {
                     hmax = std::max(hmax, c.h);
                     vmax = std::max(vmax, c.v);
                 }
+                // stb_image rejects sampling factors that do not divide the maxima ("bad H" /
+                // "bad V"): the resampler reads hmax / h samples per component sample, so a
+                // non-divisor would read past the end of the component's rows
+                for (const auto &c : comp)
+                    if (hmax % c.h != 0 || vmax % c.v != 0) return err = "bad JPEG sampling factors", false;
                 const int mx = (w + 8 * hmax - 1) / (8 * hmax), my = (h + 8 * vmax - 1) / (8 * vmax);
                 for (auto &c : comp) {
                     c.x = (w * c.h + hmax - 1) / hmax;

@@ -272,9 +272,7 @@ __device__ __forceinline__ bool traverse4(const DeviceScene &sc, const RayPre &r
         while ((uint32_t)node < (uint32_t)kSentinel) {
             const Bvh4Node n = sc.nodes4[node];
             if (STATS) nodes_visited++;
-            const float sx = __uint_as_float((n.exps & 0xFFu) << 23);
-            const float sy = __uint_as_float(((n.exps >> 8) & 0xFFu) << 23);
-            const float sz = __uint_as_float(((n.exps >> 16) & 0xFFu) << 23);
+            const float sx = n.sx, sy = n.sy, sz = n.sz;
             float t[4];
             int l[4];
 #pragma unroll
@@ -468,6 +466,14 @@ struct RingStack {
     }
 };
 
+// Child order of a BVH4 visit (A/B, PUPIL_SORT at build time): 5 = full sort (the
+// nearest child is descended, the others pushed far to near); 4 = nearest first and
+// farthest pushed first, the middle two unordered; 3 = nearest first only.  Only the
+// traversal order changes: hits are resolved by the (t, id) total order either way.
+#ifndef PUPIL_SORT
+#define PUPIL_SORT 5
+#endif
+
 // Branch-free compare-exchange (selects, no divergent swap blocks).
 __device__ __forceinline__ void csel(float &ta, int &la, float &tb, int &lb) {
     const bool c = tb < ta;
@@ -558,9 +564,7 @@ template <bool PAD>
 __device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, float pad, float tmin, float tmax,
                                        float t[4], int l[4]) {
     constexpr float kInf = __builtin_huge_valf();
-    const float sx = __uint_as_float((n.exps & 0xFFu) << 23);
-    const float sy = __uint_as_float(((n.exps >> 8) & 0xFFu) << 23);
-    const float sz = __uint_as_float(((n.exps >> 16) & 0xFFu) << 23);
+    const float sx = n.sx, sy = n.sy, sz = n.sz;
     const bool px = ridir.x >= 0.f, py = ridir.y >= 0.f, pz = ridir.z >= 0.f;
     const uint32_t nx = px ? n.qlo_x : n.qhi_x, fx = px ? n.qhi_x : n.qlo_x;
     const uint32_t ny = py ? n.qlo_y : n.qhi_y, fy = py ? n.qhi_y : n.qlo_y;
@@ -582,8 +586,19 @@ __device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, f
     csel(t[0], l[0], t[1], l[1]);
     csel(t[2], l[2], t[3], l[3]);
     csel(t[0], l[0], t[2], l[2]);
+#if PUPIL_SORT >= 4
     csel(t[1], l[1], t[3], l[3]);
+#endif
+#if PUPIL_SORT >= 5
     csel(t[1], l[1], t[2], l[2]);
+#endif
+}
+
+// Node fetch by a 32-bit byte offset from the uniform base (the engine keeps node
+// arrays to at most 2^26 nodes = 4 GiB, kMaxNodes4), which the compiler turns into
+// SGPR-base + VGPR-offset loads: one VALU op per visit instead of a 64-bit shift and add.
+__device__ __forceinline__ Bvh4Node load_node4(const DeviceScene &sc, int node) {
+    return *reinterpret_cast<const Bvh4Node *>(reinterpret_cast<const char *>(sc.nodes4) + ((uint32_t)node << 6));
 }
 
 // Two-level: the object-space box ray of instance `in` (origin, reciprocal
@@ -766,7 +781,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         // ---- traverse until this lane's ray terminates or it needs a leaf while others do too
         if (active) {
             while ((uint32_t)node < (uint32_t)kSentinel) {
-                const Bvh4Node n = sc.nodes4[node];
+                const Bvh4Node n = load_node4(sc, node);
                 if (STATS) {
                     if (kMixed && any) nv_sh++;
                     else nv++;

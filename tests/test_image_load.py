@@ -243,6 +243,60 @@ def test_exr_rejections(tmp_path):
     assert load(tmp_path / "x.png")[0] == abi.ERR_IO
 
 
+def test_exr_corrupt_files_fail_cleanly(tmp_path):
+    """Untrusted texture files (scene XML names them): a chunk offset near 2^64, a chunk
+    size running past the end, an attribute name without its terminator and a data
+    window that overflows 32 bits are rejected with PUPIL_ERR_IO, never read past the
+    buffer (the offset arithmetic used to wrap, and names were read up to any NUL)."""
+    w, h = 4, 3
+    z = np.zeros((h, w), np.float32)
+    write_exr(tmp_path / "ok.exr", {"R": z, "G": z, "B": z}, w, h)
+    good = bytearray((tmp_path / "ok.exr").read_bytes())
+    assert load(tmp_path / "ok.exr")[0] == 0
+    # the offset table follows the header's terminating NUL: find the first chunk offset
+    first_off = len(good) - h * (8 + 3 * 4 * w)
+    at = good.index(struct.pack("<Q", first_off))
+    for bad_off in (2 ** 64 - 4, 2 ** 64 - 16, len(good) - 4):
+        b = bytearray(good)
+        b[at:at + 8] = struct.pack("<Q", bad_off)
+        (tmp_path / "off.exr").write_bytes(bytes(b))
+        assert load(tmp_path / "off.exr")[0] == abi.ERR_IO, bad_off
+    b = bytearray(good)  # chunk size field: 2^31 - 1 bytes
+    b[first_off + 4:first_off + 8] = struct.pack("<i", 2 ** 31 - 1)
+    (tmp_path / "size.exr").write_bytes(bytes(b))
+    assert load(tmp_path / "size.exr")[0] == abi.ERR_IO
+    # header cut inside an attribute name (no NUL before the end of the file)
+    (tmp_path / "name.exr").write_bytes(bytes(good[:8]) + b"channelsXXXXXXXXXXXXXXXXXXXXXXXXXXXX")
+    assert load(tmp_path / "name.exr")[0] == abi.ERR_IO
+    # data window spanning more than 2^31 columns
+    b = bytearray(good)
+    dwa = b.index(b"dataWindow\0box2i\0") + len(b"dataWindow\0box2i\0") + 4
+    b[dwa:dwa + 16] = struct.pack("<iiii", -2 ** 31, 0, 2 ** 31 - 1, h - 1)
+    (tmp_path / "dw.exr").write_bytes(bytes(b))
+    assert load(tmp_path / "dw.exr")[0] == abi.ERR_IO
+    for n in range(8, len(good), 7):  # every truncation fails cleanly
+        (tmp_path / "cut.exr").write_bytes(bytes(good[:n]))
+        assert load(tmp_path / "cut.exr")[0] == abi.ERR_IO, n
+
+
+def test_jpeg_sampling_factors_must_divide_the_maxima(tmp_path):
+    """stb_image rejects a component whose sampling factor does not divide the largest
+    one ("bad H" / "bad V"); the decoder must too (its resampler would read past the
+    component's rows)."""
+    arr = np.random.default_rng(3).integers(0, 256, (32, 32, 3), dtype=np.uint8)
+    PIL.fromarray(arr, "RGB").save(tmp_path / "a.jpg", quality=90, subsampling=2)
+    data = bytearray((tmp_path / "a.jpg").read_bytes())
+    assert load(tmp_path / "a.jpg")[0] == 0
+    sof = data.index(b"\xff\xc0")
+    comps = sof + 2 + 2 + 1 + 2 + 2 + 1  # marker, length, precision, height, width, count
+    for y_hv, c_hv in ((0x41, 0x31), (0x14, 0x13), (0x44, 0x33)):
+        b = bytearray(data)
+        b[comps + 1] = y_hv      # Y: h, v
+        b[comps + 3 + 1] = c_hv  # Cb: a factor that does not divide Y's
+        (tmp_path / "bad.jpg").write_bytes(bytes(b))
+        assert load(tmp_path / "bad.jpg")[0] == abi.ERR_IO, hex(c_hv)
+
+
 def write_hdr(path, rgbe, rle=True):
     h, w, _ = rgbe.shape
     out = bytearray(b"#?RADIANCE\n# made by the test\nFORMAT=32-bit_rle_rgbe\n\n" + f"-Y {h} +X {w}\n".encode())
