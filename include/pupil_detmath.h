@@ -26,6 +26,29 @@
 
 namespace pupil_dm {
 
+/* PUPIL_FASTMATH_EMULATION (host only; oracle/Makefile liboracle_fastmath.so, test
+ * infrastructure for tools/fastmath_sensitivity.py -- never the engine): the error
+ * model of CUDA -use_fast_math, which the reference is compiled with
+ * (CMakeLists.txt:45).  Each result is displaced deterministically (a hash of the
+ * input) by up to the documented maximum error: __sinf / __cosf 2^-21.41 absolute,
+ * acosf 2 ulp, atan2f 3 ulp (CUDA C Programming Guide, Mathematical Functions). */
+#if defined(PUPIL_FASTMATH_EMULATION) && !defined(__HIP_DEVICE_COMPILE__)
+inline float dm_fm_noise(float x, unsigned salt) {
+    unsigned u;
+    __builtin_memcpy(&u, &x, 4);
+    u = (u ^ (salt * 0x9e3779b9u)) * 0x85ebca6bu;
+    u ^= u >> 13;
+    u *= 0xc2b2ae35u;
+    u ^= u >> 16;
+    return (float)(int)u * (1.0f / 2147483648.0f); /* [-1, 1) */
+}
+#define PUPIL_DM_FM_ABS(v, x, salt, err) ((v) + (err) * pupil_dm::dm_fm_noise((x), (salt)))
+#define PUPIL_DM_FM_ULP(v, x, salt, ulps) ((v) * (1.0f + (ulps) * 5.9604645e-8f * pupil_dm::dm_fm_noise((x), (salt))))
+#else
+#define PUPIL_DM_FM_ABS(v, x, salt, err) (v)
+#define PUPIL_DM_FM_ULP(v, x, salt, ulps) (v)
+#endif
+
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kPiOver2 = 1.57079632679489661923f;
 constexpr float kPiOver4 = 0.785398163397448309616f;
@@ -65,6 +88,8 @@ PUPIL_DM_HD void dm_sincos(float x, float &s, float &c) {
         case 2: s = -ps; c = -pc; break;
         default: s = -pc; c = ps; break;
     }
+    s = PUPIL_DM_FM_ABS(s, x, 1u, 3.6e-7f);
+    c = PUPIL_DM_FM_ABS(c, x, 2u, 3.6e-7f);
 }
 
 PUPIL_DM_HD float dm_sin(float x) { float s, c; dm_sincos(x, s, c); return s; }
@@ -97,7 +122,7 @@ PUPIL_DM_HD float dm_asin(float x) {
     return sign * p;
 }
 
-PUPIL_DM_HD float dm_acos(float x) {
+PUPIL_DM_HD float dm_acos_exact(float x) {
     if (x < -0.5f) {
         float h = 0.5f * (1.0f + x);
         return kPi - 2.0f * dm_asin(sqrtf(h));
@@ -108,6 +133,8 @@ PUPIL_DM_HD float dm_acos(float x) {
     }
     return kPiOver2 - dm_asin(x);
 }
+
+PUPIL_DM_HD float dm_acos(float x) { return PUPIL_DM_FM_ULP(dm_acos_exact(x), x, 3u, 2.0f); }
 
 /* atan for any finite x (Cephes atanf structure) */
 PUPIL_DM_HD float dm_atan(float x) {
@@ -133,7 +160,7 @@ PUPIL_DM_HD float dm_atan(float x) {
 }
 
 /* atan2 with the libm quadrant conventions (atan2(±0, +0) = ±0, atan2(±0, -0) = ±pi) */
-PUPIL_DM_HD float dm_atan2(float y, float x) {
+PUPIL_DM_HD float dm_atan2_exact(float y, float x) {
     if (x == 0.f) {
         if (y > 0.f) return kPiOver2;
         if (y < 0.f) return -kPiOver2;
@@ -146,5 +173,7 @@ PUPIL_DM_HD float dm_atan2(float y, float x) {
     }
     return z;
 }
+
+PUPIL_DM_HD float dm_atan2(float y, float x) { return PUPIL_DM_FM_ULP(dm_atan2_exact(y, x), y + x, 4u, 3.0f); }
 
 }  // namespace pupil_dm

@@ -271,6 +271,13 @@ typedef struct pupil_pt_counters {
     /* two-level structure: TLAS nodes whose children were chosen by the binned SAH (an
      * entry range too large for the exact split search, accel_two_level.hip) */
     uint64_t tlas_sah_splits;
+    /* collect_stats, persistent traversal kernels: list items the dequeue heads handed
+     * out, lanes activated with them, lanes retired, and the launches' list lengths --
+     * all four equal when no ray is lost or traced twice */
+    uint64_t queue_handed;
+    uint64_t queue_activated;
+    uint64_t queue_retired;
+    uint64_t queue_listed;
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;

@@ -1762,7 +1762,19 @@ int oracle_render(oracle_scene *s, uint32_t random_seed, uint32_t sample_cnt, ui
         c3 += counts[3];
     };
     std::vector<std::thread> pool;
+#if defined(PUPIL_FASTMATH_EMULATION)
+    // -ftz=true of -use_fast_math: denormal results flush to zero, denormal inputs read as zero
+    auto ftz_worker = [&]() {
+        unsigned csr;
+        __asm__ volatile("stmxcsr %0" : "=m"(csr));
+        csr |= 0x8040u;  // FTZ | DAZ
+        __asm__ volatile("ldmxcsr %0" : : "m"(csr));
+        worker();
+    };
+    for (int t = 0; t < threads; t++) pool.emplace_back(ftz_worker);
+#else
     for (int t = 0; t < threads; t++) pool.emplace_back(worker);
+#endif
     for (auto &t : pool) t.join();
     const auto t1 = std::chrono::steady_clock::now();
     if (stats) {

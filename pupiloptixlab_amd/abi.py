@@ -90,7 +90,9 @@ class Counters(C.Structure):
                 ("bvh_depth", C.c_uint64), ("unique_node_fetches", C.c_uint64),
                 # ABI 3
                 ("rays_traced_total", C.c_uint64), ("frames_in_flight", C.c_uint64),
-                ("pipeline_slots", C.c_uint64), ("tlas_sah_splits", C.c_uint64)]
+                ("pipeline_slots", C.c_uint64), ("tlas_sah_splits", C.c_uint64),
+                ("queue_handed", C.c_uint64), ("queue_activated", C.c_uint64), ("queue_retired", C.c_uint64),
+                ("queue_listed", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -1216,6 +1216,10 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
             c.prim_tests = tc[1] + tc[15];
             c.shadow_rays_reference = tc[16];
             c.unique_node_fetches = tc[18];
+            c.queue_handed = tc[20];
+            c.queue_activated = tc[21];
+            c.queue_retired = tc[22];
+            c.queue_listed = tc[23];
             c.extend_node_visits = tc[0];
             c.extend_prim_tests = tc[1];
             const double rays = (double)(c.primary_rays + c.extension_rays + c.shadow_rays);
@@ -1258,12 +1262,28 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
     HIP_TRY(hipMalloc((void **)&d_rays, sizeof(float) * 8 * (size_t)n));
     hipError_t e = hipMalloc((void **)&d_out, sizeof(float) * 4 * (size_t)n);
     if (e == hipSuccess) e = hipMemcpy(d_rays, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice);
+    // PUPIL_TRACE_RAYS_STATS: the counter kernels (queue accounting, node visits), read back
+    // by pupil_pt_stats like a collect_stats render's
+    const bool stats = std::getenv("PUPIL_TRACE_RAYS_STATS") != nullptr;
+    TraceStats ts{pt->trace_counters};
     if (e == hipSuccess) {
         e = hipMemsetAsync(pt->q.work + kWorkRays, 0, kWorkKind * sizeof(uint32_t), pt->own_stream);
+        if (e == hipSuccess && stats) e = hipMemsetAsync(pt->trace_counters, 0, 32 * sizeof(unsigned long long), pt->own_stream);
+        if (e == hipSuccess) e = hipEventRecord(pt->ev_begin, pt->own_stream);
         if (e == hipSuccess)
             launch_trace_debug(pt->sc, d_rays, d_out, n, any_hit, pt->ovf, pt->ovf_threads, pt->q.work + kWorkRays,
-                               pt->own_stream);
-        e = hipStreamSynchronize(pt->own_stream);
+                               pt->own_stream, stats ? &ts : nullptr);
+        if (e == hipSuccess) e = hipEventRecord(pt->ev_end, pt->own_stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(pt->own_stream);
+    }
+    if (e == hipSuccess && stats) {
+        pt->last_paths = n;
+        pt->last_iters = 0;
+        pt->last_primary = n;
+        pt->last_stats = true;
+        pt->trace_pairs = 0;
+        pt->rendered = true;
+        pt->last_stream = pt->own_stream;
     }
     if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(float) * 4 * (size_t)n, hipMemcpyDeviceToHost);
     (void)hipFree(d_rays);

@@ -12,7 +12,10 @@ namespace pupil {
 
 constexpr int kTraceBlock = 128;
 constexpr int kTraceWavesPerSimd = 7;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8: 2 % slower)
-constexpr int kTraceWavesPerSimd8 = 5;  // BVH8 kernels (<= 96 VGPRs; 6 waves spill 17 registers: 24.2 vs 23.7 ms)
+#ifndef PUPIL_W8_WAVES  // A/B builds only (tools/dbg: the spilled 6-wave BVH8 kernels)
+#define PUPIL_W8_WAVES 5
+#endif
+constexpr int kTraceWavesPerSimd8 = PUPIL_W8_WAVES;  // BVH8 kernels (<= 96 VGPRs; 6 waves spill 17 registers: 24.2 vs 23.7 ms)
 constexpr int kTraceWavesPerSimdTL = 5;  // two-level variant (<= 96 VGPRs; A/B r02 on config 5: 4 waves 688, 5: 743, 6: 716 Mrays/s)
 constexpr int kStackLds = 32;   // per-thread LDS stack entries
 constexpr int kStackOvf = 160;  // per-thread global overflow entries
@@ -111,7 +114,8 @@ struct FrameParams {
 
 struct TraceStats {
     unsigned long long *counters;  // [0..1] closest-hit nodes/prims, [14..15] shadow, [2..13] diagnostics,
-                                   // [16] reference shadow rays, [18] distinct node fetches
+                                   // [16] reference shadow rays, [18] distinct node fetches,
+                                   // [20..23] queue accounting (handed, activated, retired, listed)
     // PUPIL_TRACE_TAIL diagnostics (STATS kernels only, else null): per wave of the
     // persistent launch, s_memrealtime (100 MHz) at start, when its dequeue found
     // the work list drained, at exit, and the rays it took
@@ -152,8 +156,9 @@ void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues
 void launch_accumulate(const FrameParams &fp, const PathState &ps, const float *aov_src, bool clear_flags,
                        hipStream_t s);
 uint32_t trace_grid_blocks();
+// stats (or null): the persistent kernels' counter variants (queue accounting, node visits)
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
-                        uint32_t ovf_threads, uint32_t *work, hipStream_t s);
+                        uint32_t ovf_threads, uint32_t *work, hipStream_t s, const TraceStats *stats = nullptr);
 void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, hipStream_t s);
 // device emitter selection for n random numbers: area index, -1 env, -2 none
 void launch_debug_select(const DeviceScene &sc, const float *p, int *out, uint32_t n, hipStream_t s);

@@ -658,6 +658,10 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     // theirs is exhausted, so every item is taken exactly once.
     uint32_t shard = blockIdx.x % kWorkShards, tried = 0;
     unsigned long long t_start = 0, t_drained = 0, n_taken = 0;  // PUPIL_TRACE_TAIL
+    // STATS: queue accounting of this wave (wave-uniform): list items the dequeue heads
+    // handed it, lanes it activated, lanes it retired (counters[20..22]; every launch
+    // must give handed = activated = retired = its list length, counters[23])
+    uint32_t q_handed = 0, q_act = 0, q_ret = 0;
     if (STATS && stats.wave_times) t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t p = 0, best_key = 0, best_idx = kMissIndex;
     RayPre r{};
@@ -702,6 +706,8 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 dg[5] += min(n_idle, base < len ? len - base : 0u);
             }
             if (STATS) n_taken += min(n_idle, base < len ? len - base : 0u);
+            if (STATS) q_handed += min(n_idle, base < len ? len - base : 0u);
+            const bool was_active = active;
             if (base + n_idle >= len) {  // chunk exhausted: continue on the next one
                 shard = shard + 1 == kWorkShards ? 0u : shard + 1;
                 if (++tried == kWorkShards) {
@@ -773,6 +779,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     active = true;
                 }
             }
+            if (STATS) q_act += (uint32_t)__popcll(__ballot(active && !was_active));
         }
         if (!__any(active)) {
             if (drained) break;
@@ -922,6 +929,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             o[2] = b2;
             o[3] = __uint_as_float(found && !ANY ? best_key : 0xFFFFFFFFu);
         }
+        if (STATS) q_ret += (uint32_t)__popcll(__ballot(done));
         if (done) active = false;
     }
     flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
@@ -943,9 +951,16 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         const uint32_t sub = blockIdx.x % kWorkShards;
         const uint32_t groups = min(gridDim.x, kWorkShards);
         const uint32_t sub_waves = (gridDim.x - sub + kWorkShards - 1u) / kWorkShards * (blockDim.x / 64u);
+        if (STATS) {
+            atomicAdd(&stats.counters[20], (unsigned long long)q_handed);
+            atomicAdd(&stats.counters[21], (unsigned long long)q_act);
+            atomicAdd(&stats.counters[22], (unsigned long long)q_ret);
+        }
         if (atomicAdd(job.work + (kWorkShards + 1u + sub) * kWorkStride, 1u) == sub_waves - 1u &&
-            atomicAdd(job.work + kWorkShards * kWorkStride, 1u) == groups - 1u)
+            atomicAdd(job.work + kWorkShards * kWorkStride, 1u) == groups - 1u) {
             for (uint32_t k = 0; k < 2u * kWorkShards + 1u; k++) atomicExch(job.work + k * kWorkStride, 0u);
+            if (STATS) atomicAdd(&stats.counters[23], (unsigned long long)(count + n_ahead));  // once per launch
+        }
     }
     if (STATS) {
         for (int k = 0; k < 6; k++) {
@@ -1095,6 +1110,7 @@ __device__ __forceinline__ void trace8_body(const DeviceScene &sc, const PathSta
     bool active = false, drained = false;
     uint32_t shard = blockIdx.x % kWorkShards, tried = 0;
     unsigned long long t_start = 0, t_drained = 0, n_taken = 0;
+    uint32_t q_handed = 0, q_act = 0, q_ret = 0;  // STATS queue accounting, as trace4_body
     if (STATS && stats.wave_times) t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t p = 0, best_key = 0, best_idx = kMissIndex;
     RayPre r{};
@@ -1126,6 +1142,8 @@ __device__ __forceinline__ void trace8_body(const DeviceScene &sc, const PathSta
                 dg[5] += min(n_idle, base < len ? len - base : 0u);
             }
             if (STATS) n_taken += min(n_idle, base < len ? len - base : 0u);
+            if (STATS) q_handed += min(n_idle, base < len ? len - base : 0u);
+            const bool was_active = active;
             if (base + n_idle >= len) {
                 shard = shard + 1 == kWorkShards ? 0u : shard + 1;
                 if (++tried == kWorkShards) {
@@ -1180,6 +1198,7 @@ __device__ __forceinline__ void trace8_body(const DeviceScene &sc, const PathSta
                     active = true;
                 }
             }
+            if (STATS) q_act += (uint32_t)__popcll(__ballot(active && !was_active));
         }
         if (!__any(active)) {
             if (drained) break;
@@ -1319,6 +1338,7 @@ __device__ __forceinline__ void trace8_body(const DeviceScene &sc, const PathSta
             o[2] = b2;
             o[3] = __uint_as_float(found && !ANY ? best_key : 0xFFFFFFFFu);
         }
+        if (STATS) q_ret += (uint32_t)__popcll(__ballot(done));
         if (done) active = false;
     }
     flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
@@ -1335,9 +1355,16 @@ __device__ __forceinline__ void trace8_body(const DeviceScene &sc, const PathSta
         const uint32_t sub = blockIdx.x % kWorkShards;
         const uint32_t groups = min(gridDim.x, kWorkShards);
         const uint32_t sub_waves = (gridDim.x - sub + kWorkShards - 1u) / kWorkShards * (blockDim.x / 64u);
+        if (STATS) {
+            atomicAdd(&stats.counters[20], (unsigned long long)q_handed);
+            atomicAdd(&stats.counters[21], (unsigned long long)q_act);
+            atomicAdd(&stats.counters[22], (unsigned long long)q_ret);
+        }
         if (atomicAdd(job.work + (kWorkShards + 1u + sub) * kWorkStride, 1u) == sub_waves - 1u &&
-            atomicAdd(job.work + kWorkShards * kWorkStride, 1u) == groups - 1u)
+            atomicAdd(job.work + kWorkShards * kWorkStride, 1u) == groups - 1u) {
             for (uint32_t k = 0; k < 2u * kWorkShards + 1u; k++) atomicExch(job.work + k * kWorkStride, 0u);
+            if (STATS) atomicAdd(&stats.counters[23], (unsigned long long)count);  // once per launch
+        }
     }
     if (STATS) {
         for (int k = 0; k < 6; k++) {
@@ -1862,30 +1889,14 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
 }
 
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
-                        uint32_t ovf_threads, uint32_t *work, hipStream_t s) {
+                        uint32_t ovf_threads, uint32_t *work, hipStream_t s, const TraceStats *stats) {
     if ((sc.bvh_width == 4 || sc.bvh_width == 8) && sc.trace_refill) {  // the production kernel, fed from a ray array
         const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, sc.trace_node_min, rays, out, 0u, 0u};
-        const uint32_t blocks = trace4_blocks(sc, ovf_threads);
-        if (sc.bvh_width == 8) {
-            if (any)
-                hipLaunchKernelGGL((k_trace8<kModeRays, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
-                                   PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
-            else
-                hipLaunchKernelGGL((k_trace8<kModeRays, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
-                                   PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
-        } else if (sc.two_level && !sc.tl_world) {
-            if (any)
-                hipLaunchKernelGGL((k_trace4tl<kModeRays, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
-                                   PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
-            else
-                hipLaunchKernelGGL((k_trace4tl<kModeRays, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
-                                   PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
-        } else if (any)
-            hipLaunchKernelGGL((k_trace4<kModeRays, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
-                               PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
+        const Queues q{};
+        if (any)
+            launch_trace4<kModeRays, true>(sc, PathState{}, q, job, ovf, ovf_threads, stats, s);
         else
-            hipLaunchKernelGGL((k_trace4<kModeRays, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc,
-                               PathState{}, Queues{}, job, ovf, ovf_threads, TraceStats{nullptr});
+            launch_trace4<kModeRays, false>(sc, PathState{}, q, job, ovf, ovf_threads, stats, s);
         return;
     }
     const uint32_t blocks = std::min((n + kTraceBlock - 1) / kTraceBlock, std::max(1u, ovf_threads / kTraceBlock));

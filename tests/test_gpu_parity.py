@@ -880,3 +880,48 @@ def test_shade_list_modes_parity(mode, monkeypatch):
     s, rs = gpu["stats"], ref["stats"]
     assert (s["extension_rays"], s["shadow_rays"], s["shadow_rays_reference"]) == \
         (rs["extension_rays"], rs["shadow_rays"], rs["shadow_rays_reference"])
+
+
+@pytest.mark.parametrize("family", ["bvh4", "two_level_world", "two_level_object", "bvh8", "bvh8_refill1"])
+def test_persistent_queue_accounting(family, monkeypatch):
+    """Every persistent traversal family hands out each listed ray exactly once: per
+    launch, the items the XCD dequeue heads handed out = the lanes activated with them =
+    the lanes retired = the list length, summed over a counter render (primary extend +
+    mixed launches) and over closest-hit and any-hit ray queries.  (A round-2 experiment
+    with the spilled 6-wave BVH8 kernel once left whole 64-ray batches untraced; this is
+    the check that would catch it in any family.)"""
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    if family == "bvh8" or family == "bvh8_refill1":
+        monkeypatch.setenv("PUPIL_BVH_WIDTH", "8")
+    if family == "bvh8_refill1":
+        monkeypatch.setenv("PUPIL_REFILL", "1")
+    if family.startswith("two_level"):
+        monkeypatch.setenv("PUPIL_ACCEL", "two_level")
+        monkeypatch.setenv("PUPIL_TL_MODE", "world" if family == "two_level_world" else "object")
+    w = scenes.sphere_field(27, 64, 36, 4, seed=9)
+    desc = w.desc()
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    pt.render(4, collect_stats=1)
+    c = pt.stats()
+    rays = c["primary_rays"] + c["extension_rays"] + c["shadow_rays"]
+    assert (c["queue_handed"], c["queue_activated"], c["queue_retired"], c["queue_listed"]) == (rays,) * 4, c
+    rng = np.random.default_rng(11)
+    n = 200000
+    org = rng.uniform([-7.5, 0.1, -9.5], [7.5, 13.9, 13.5], (n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r8 = np.ascontiguousarray(np.concatenate([org, d, np.full((n, 1), 0.001), np.full((n, 1), 1e16)], 1), np.float32)
+    ref = oracle.OracleScene(desc).closest(r8[:, :6])
+    monkeypatch.setenv("PUPIL_TRACE_RAYS_STATS", "1")
+    for any_hit in (0, 1):
+        out = np.full((n, 4), np.nan, np.float32)
+        abi.check(pt._lib.pupil_pt_trace_rays(pt._pt, n, r8.ctypes.data_as(abi.f32p), out.ctypes.data_as(abi.f32p),
+                                              any_hit))
+        c = pt.stats()
+        assert (c["queue_handed"], c["queue_activated"], c["queue_retired"], c["queue_listed"]) == (n,) * 4, \
+            (any_hit, c["queue_handed"], c["queue_activated"], c["queue_retired"], c["queue_listed"])
+        assert not np.isnan(out).any()  # every ray's record written
+        assert np.array_equal(out[:, 0] > 0, ref[:, 0] > 0)
+    pt.close_engine()
