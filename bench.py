@@ -30,7 +30,6 @@ sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
 
-
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,7 +69,6 @@ def parse():
     args.max_depth = depth if args.max_depth is None else args.max_depth
     args.cpu_sample_stride = stride if args.cpu_sample_stride is None else args.cpu_sample_stride
     return args
-
 
 def main():
     args = parse()
@@ -212,18 +210,6 @@ def main():
     # bytes (per-ray figures of the committed PMC passes of this config, times this
     # rank's rays per launch).  Launch time: HIP events around the timed steps' launches.
     roof = roofline(args, st_bytes, timed) if rank == 0 else None
-    update = None
-    if args.config == 5 and rank == 0:  # RenderInstanceUpdate cost: move instance 0, re-sync the accel
-        from pupiloptixlab_amd import world as W
-
-        t0 = time.perf_counter()
-        scene.set_instance_transform(0, W.transform(translate=(0.25, 0.0, 0.0)) @
-                                     np.asarray(scene.desc().instances[0].to_world[:] + [0, 0, 0, 1],
-                                                np.float32).reshape(4, 4))
-        pt.update_instance(scene, 0)
-        torch.cuda.synchronize(dev)
-        update = {"host_ms": round((time.perf_counter() - t0) * 1e3, 3), "engine_ms": round(pt.stats()["build_ms"], 3)}
-
     dropin = None
     if rank == 0 and world == 1 and args.dropin and args.config in (3, 4) and args.emissive_groups == 0:
         dropin = dropin_cadence(args, ms_per_step, last_accum)
@@ -233,6 +219,20 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline and args.emissive_groups == 0:
         cpu = cpu_baseline(desc, args, pt)
         timed_check = timed_frame_check(desc, args, last_accum, seed_t0 + args.steps * args.spp)
+
+    # RenderInstanceUpdate cost (config 5): move instance 0, re-sync the accel.  Last: the
+    # checks above compare the frames rendered before the move with the unmoved scene
+    update = None
+    if args.config == 5 and rank == 0:
+        from pupiloptixlab_amd import world as W
+
+        t0 = time.perf_counter()
+        scene.set_instance_transform(0, W.transform(translate=(0.25, 0.0, 0.0)) @
+                                     np.asarray(scene.desc().instances[0].to_world[:] + [0, 0, 0, 1],
+                                                np.float32).reshape(4, 4))
+        pt.update_instance(scene, 0)
+        torch.cuda.synchronize(dev)
+        update = {"host_ms": round((time.perf_counter() - t0) * 1e3, 3), "engine_ms": round(pt.stats()["build_ms"], 3)}
 
     if rank == 0:
         if args.dump:
@@ -308,7 +308,6 @@ def main():
     if world > 1:
         dist.destroy_process_group()
 
-
 def dropin_cadence(args, batched_ms, last_accum):
     """The reference's cadence through the C++ drop-in: examples/path_tracer (System +
     PTPass, pt_pass.cpp:39-57: one 1-spp render per OnRun, then a stream sync) on this
@@ -346,12 +345,10 @@ def dropin_cadence(args, batched_ms, last_accum):
                    "exported XML; bit_exact: its final accumulation vs the bench's last timed frame (same seeds)")
     return rec
 
-
 def default_config(args):
     defaults = {3: (125, 1920, 1080, 8, 4), 4: (500, 1920, 1080, 8, 4), 5: (125, 3840, 2160, 16, 6)}
     return (args.spheres, args.width, args.height, args.spp, args.max_depth) == defaults[args.config] and \
         args.emissive_groups == 0
-
 
 def pmc_record(args):
     """Per-ray PMC figures of the plain k_trace4 launches for this config (tools/gpu_pmc.sh
@@ -370,7 +367,6 @@ def pmc_record(args):
         return None
     return rec if rec.get("traffic_bytes_per_ray") else None
 
-
 def gather_ceiling(footprint_bytes):
     """Dependent random 64-B gather ceiling of this GPU (G fetches/s), measured now by
     build/ubench_gather on a table of the next power of two above the traversal's
@@ -387,7 +383,6 @@ def gather_ceiling(footprint_bytes):
         return json.loads(r.stdout.strip().splitlines()[-1])
     except (OSError, ValueError, IndexError, subprocess.SubprocessError):
         return None
-
 
 def roofline(args, st_bytes, timed):
     """st_bytes: the counter frame's stats (per-ray node visits, primitive tests, bytes);
@@ -454,7 +449,6 @@ def roofline(args, st_bytes, timed):
     keys = ["bound", "achieved", "peak", "unit", "frac", "traffic"]
     return {**{k: out[k] for k in keys}, **{k: v for k, v in out.items() if k not in keys}}
 
-
 def usable_cpus():
     """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota."""
     n = len(os.sched_getaffinity(0))
@@ -466,7 +460,6 @@ def usable_cpus():
         except (OSError, ValueError):
             pass
     return n
-
 
 def native_oracle():
     """Build the oracle for THIS host (-O3 -march=native, same -ffp-contract=off, no
@@ -484,7 +477,6 @@ def native_oracle():
         return out
     except (OSError, subprocess.SubprocessError):
         return None
-
 
 def timed_frame_check(desc, args, last_accum, n_frames):
     """The last timed frame (a progressive render of seeds 0 .. n_frames - 1, most of it
@@ -506,7 +498,6 @@ def timed_frame_check(desc, args, last_accum, n_frames):
     exact = int(np.all(gpu.view(np.uint32) == r["accum"].view(np.uint32), axis=1).sum())
     return {"pixels": f"every {stride}th pixel from {stride // 2}", "frames": int(n_frames),
             "bit_exact": f"{exact}/{len(pixels)}"}
-
 
 def cpu_baseline(desc, args, pt):
     """The CPU oracle (scalar C++ restatement of the same integrator, traversing the
@@ -554,7 +545,6 @@ def cpu_baseline(desc, args, pt):
                     "traverses, near-to-far order, the GPU's conservative quantized box test)") if exported is not None
             else "the oracle's own binned-SAH BVH2 (two-level scene: no flattened BVH4 to export)",
             "gpu_pixels_bit_exact": f"{exact}/{len(pixels)}"}
-
 
 if __name__ == "__main__":
     main()
