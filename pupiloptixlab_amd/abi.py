@@ -169,7 +169,7 @@ def load_library(path: str | None = None):
         import torch  # noqa: F401
     except Exception:  # pragma: no cover - torch is optional for host-only use
         pass
-    # PUPIL_LIB: an alternative build of the same library (A/B experiments, tools/gpu_ab_lib.sh)
+    # PUPIL_LIB: an alternative build of the same library (A/B experiments, tools/gpu_lib_sweep.sh)
     p = path or os.environ.get("PUPIL_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise FileNotFoundError(f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")

@@ -1,0 +1,518 @@
+// pt_traverse.h — device code shared by the traversal kernels of pt_kernels.hip
+// (the production persistent BVH4 kernels) and pt_kernels_alt.hip (the A/B
+// families: one-ray-per-lane BVH2 / BVH4 kernels, the persistent BVH8 kernels,
+// the ray-query verification kernel): stacks, leaf tests, the persistent-kernel
+// job descriptor and the quantized BVH4 box test.
+#pragma once
+
+#include "pt_kernels.h"
+#include "pt_shading.h"
+#include "pt_trace.h"
+
+namespace pupil {
+namespace tr {
+
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+__device__ __forceinline__ vec3 f3(float4 v) { return v3(v.x, v.y, v.z); }
+__device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
+
+// ------------------------------------------------------------------ traversal
+// Stack: kStackLds entries in LDS (lane-interleaved), overflow to HBM.
+struct Stack {
+    int *lds;          // this thread's column base
+    int *ovf;          // this thread's overflow base
+    uint32_t ovf_stride;
+    // indices are clamped to the capacity: a pathological tree can only give
+    // a wrong answer, never an out-of-bounds access
+    __device__ __forceinline__ void store(int i, int v) {
+        i = min(i, kStackLds + kStackOvf - 1);
+        if (i < kStackLds) lds[i * kTraceBlock] = v;
+        else ovf[(size_t)(i - kStackLds) * ovf_stride] = v;
+    }
+    __device__ __forceinline__ int load(int i) const {
+        i = max(0, min(i, kStackLds + kStackOvf - 1));
+        return i < kStackLds ? lds[i * kTraceBlock] : ovf[(size_t)(i - kStackLds) * ovf_stride];
+    }
+};
+
+constexpr int kSentinel = kTraverseDone;
+
+// Aila-Laine while-while traversal with postponed leaves.  ANY = shadow
+// (terminate on first hit, OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT).
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool traverse(const DeviceScene &sc, const RayPre &r, float tmin, float &tmax,
+                                         uint32_t &best_key, uint32_t &best_idx, float &bb1, float &bb2, Stack &st,
+                                         uint32_t &nodes_visited, uint32_t &prims_tested) {
+    int sp = 0;
+    st.store(0, kSentinel);
+    int node = (int)sc.root_link;
+    int leaf = 0;
+    if (node < 0) {  // the whole scene is one leaf
+        leaf = node;
+        node = kSentinel;
+    }
+    bool found = false;
+    while (node != kSentinel || leaf < 0) {
+        while ((uint32_t)node < (uint32_t)kSentinel) {
+            const BvhNode n = sc.nodes[node];
+            if (STATS) nodes_visited++;
+            const float t0 = box_entry(r, v3(n.lo0.x, n.lo0.y, n.lo0.z), v3(n.hi0.x, n.hi0.y, n.hi0.z), tmin, tmax);
+            const float t1 = box_entry(r, v3(n.lo1.x, n.lo1.y, n.lo1.z), v3(n.hi1.x, n.hi1.y, n.hi1.z), tmin, tmax);
+            const bool h0 = t0 != __builtin_huge_valf();
+            const bool h1 = t1 != __builtin_huge_valf();
+            int c0 = __float_as_int(n.lo0.w);
+            int c1 = __float_as_int(n.hi0.w);
+            if (!h0 && !h1) {
+                node = st.load(sp);
+                sp--;
+            } else {
+                node = h0 ? c0 : c1;
+                if (h0 && h1) {
+                    if (t1 < t0) {
+                        const int tmp = node;
+                        node = c1;
+                        c1 = tmp;
+                    }
+                    sp++;
+                    if (sp >= kStackLds + kStackOvf) sp = kStackLds + kStackOvf - 1;  // never reached (depth <= 62)
+                    st.store(sp, c1);
+                }
+            }
+            if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
+                leaf = node;
+                node = st.load(sp);
+                sp--;
+            }
+            if (!__any(leaf >= 0)) break;
+        }
+        while (leaf < 0) {
+            const uint32_t first = leaf_first(leaf);
+            const uint32_t count = leaf_count(leaf);
+            for (uint32_t i = first; i < first + count; i++) {
+                const float4 a = sc.prims[3 * i + 0];
+                const uint32_t ref = __float_as_uint(a.w);
+                const uint32_t key = ref & ~kPrimSphereBit;
+                if (STATS) prims_tested++;
+                float t, b1 = 0.f, b2 = 0.f;
+                bool hit;
+                if (ref & kPrimSphereBit) {
+                    const float4 b = sc.prims[3 * i + 1];
+                    const DevInstance &in = sc.instances[__float_as_uint(b.w)];
+                    hit = intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, t);
+                } else {
+                    const float4 b = sc.prims[3 * i + 1];
+                    const float4 c = sc.prims[3 * i + 2];
+                    hit = intersect_triangle(r, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), tmin, tmax, t,
+                                             b1, b2);
+                }
+                if (hit) {
+                    if (ANY) {
+                        found = true;
+                        break;
+                    }
+                    if (t < tmax || key < best_key) {
+                        tmax = t;
+                        best_key = key;
+                        best_idx = i;
+                        bb1 = b1;
+                        bb2 = b2;
+                        found = true;
+                    }
+                }
+            }
+            if (ANY && found) break;
+            leaf = node;
+            if (node < 0) {
+                node = st.load(sp);
+                sp--;
+            }
+        }
+        if (ANY && found) break;
+    }
+    return found;
+}
+
+// Leaf intersection shared by both node formats.  any = terminate on the first
+// hit (shadow ray); a compile-time constant except in the mixed persistent kernel.
+template <bool STATS>
+__device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
+                                                   float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
+                                                   float &bb2, uint32_t &prims_tested, bool &found, bool any) {
+    const uint32_t first = leaf_first(leaf);
+    const uint32_t count = leaf_count(leaf);
+    for (uint32_t i = first; i < first + count; i++) {
+        const float4 a = sc.prims[3 * i + 0];
+        const float4 b = sc.prims[3 * i + 1];
+        const float4 c = sc.prims[3 * i + 2];
+        // the whole 48-B record in one round trip: without this the compiler sinks the
+        // vertex loads below the sphere-bit branch, a second dependent fetch per record
+        asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(c.x),
+                     "v"(c.y), "v"(c.z));
+        const uint32_t ref = __float_as_uint(a.w);
+        const uint32_t key = ref & ~kPrimSphereBit;
+        if (STATS) prims_tested++;
+        float t, b1 = 0.f, b2 = 0.f;
+        bool hit;
+        if (ref & kPrimSphereBit) {
+            const DevInstance &in = sc.instances[__float_as_uint(b.w)];
+            hit = intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, t);
+        } else {
+            hit = intersect_triangle(r, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), tmin, tmax, t, b1,
+                                     b2);
+        }
+        if (hit) {
+            if (any) {
+                found = true;
+                return true;
+            }
+            if (t < tmax || key < best_key) {
+                tmax = t;
+                best_key = key;
+                best_idx = i;
+                bb1 = b1;
+                bb2 = b2;
+                found = true;
+            }
+        }
+    }
+    return false;
+}
+
+// Two-level BLAS leaf: object-space triangle records of instance `inst`,
+// tested in world space on fl(to_world * v) (the flattened build's and the
+// oracle's world vertices), keyed by the global primitive id.
+template <bool STATS>
+__device__ __forceinline__ bool intersect_leaf_tl(const DeviceScene &sc, const RayPre &r, int leaf, uint32_t inst,
+                                                  float tmin, float &tmax, uint32_t &best_key, uint32_t &best_idx,
+                                                  float &bb1, float &bb2, uint32_t &prims_tested, bool &found,
+                                                  bool any) {
+    // the instance's world-space records (fl(to_world * v), precomputed per instance):
+    // no per-triangle transform in the loop
+    const float4 *rec = sc.wprims + 3 * (int64_t)sc.instances[inst].wrec_delta;
+    const uint32_t first = leaf_first(leaf);
+    const uint32_t count = leaf_count(leaf);
+    for (uint32_t i = first; i < first + count; i++) {
+        const float4 a = rec[3 * i + 0];
+        const float4 b = rec[3 * i + 1];
+        const float4 c = rec[3 * i + 2];
+        const uint32_t key = __float_as_uint(a.w);
+        if (STATS) prims_tested++;
+        float t, b1 = 0.f, b2 = 0.f;
+        if (intersect_triangle(r, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), tmin, tmax, t, b1, b2)) {
+            if (any) {
+                found = true;
+                return true;
+            }
+            if (t < tmax || key < best_key) {
+                tmax = t;
+                best_key = key;
+                best_idx = key;
+                bb1 = b1;
+                bb2 = b2;
+                found = true;
+            }
+        }
+    }
+    return false;
+}
+
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool intersect_leaf(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
+                                               float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
+                                               float &bb2, uint32_t &prims_tested, bool &found) {
+    return intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, bb1, bb2, prims_tested, found, ANY);
+}
+
+__device__ __forceinline__ void cswap(float &ta, int &la, float &tb, int &lb) {
+    if (tb < ta) {
+        const float t = ta;
+        ta = tb;
+        tb = t;
+        const int l = la;
+        la = lb;
+        lb = l;
+    }
+}
+
+// 4-wide quantized traversal (same while-while / postponed-leaf structure).
+// Child boxes are decoded exactly as the builder verified them, then slab-
+// tested with the conservative test; hits are sorted near-to-far with a
+// 5-comparator network, the nearest is descended, the rest pushed.
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool traverse4(const DeviceScene &sc, const RayPre &r, float tmin, float &tmax,
+                                          uint32_t &best_key, uint32_t &best_idx, float &bb1, float &bb2, Stack &st,
+                                          uint32_t &nodes_visited, uint32_t &prims_tested) {
+    constexpr float kInf = __builtin_huge_valf();
+    int sp = 0;
+    st.store(0, kSentinel);
+    int node = (int)sc.root_link4;
+    int leaf = 0;
+    if (node < 0) {  // the whole scene is one leaf
+        leaf = node;
+        node = kSentinel;
+    }
+    bool found = false;
+    while (node != kSentinel || leaf < 0) {
+        while ((uint32_t)node < (uint32_t)kSentinel) {
+            const Bvh4Node n = sc.nodes4[node];
+            if (STATS) nodes_visited++;
+            const float sx = n.sx, sy = n.sy, sz = n.sz;
+            float t[4];
+            int l[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const vec3 lo = v3(n.ox + (float)((n.qlo_x >> (8 * k)) & 0xFFu) * sx,
+                                   n.oy + (float)((n.qlo_y >> (8 * k)) & 0xFFu) * sy,
+                                   n.oz + (float)((n.qlo_z >> (8 * k)) & 0xFFu) * sz);
+                const vec3 hi = v3(n.ox + (float)((n.qhi_x >> (8 * k)) & 0xFFu) * sx,
+                                   n.oy + (float)((n.qhi_y >> (8 * k)) & 0xFFu) * sy,
+                                   n.oz + (float)((n.qhi_z >> (8 * k)) & 0xFFu) * sz);
+                l[k] = n.child[k];
+                const float te = box_entry(r, lo, hi, tmin, tmax);
+                t[k] = l[k] != kEmptyLink ? te : kInf;
+            }
+            cswap(t[0], l[0], t[1], l[1]);
+            cswap(t[2], l[2], t[3], l[3]);
+            cswap(t[0], l[0], t[2], l[2]);
+            cswap(t[1], l[1], t[3], l[3]);
+            cswap(t[1], l[1], t[2], l[2]);
+            if (t[0] == kInf) {
+                node = st.load(sp);
+                sp--;
+            } else {
+                node = l[0];
+                if (t[3] != kInf) st.store(++sp, l[3]);
+                if (t[2] != kInf) st.store(++sp, l[2]);
+                if (t[1] != kInf) st.store(++sp, l[1]);
+            }
+            if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
+                leaf = node;
+                node = st.load(sp);
+                sp--;
+            }
+            if (!__any(leaf >= 0)) break;
+        }
+        while (leaf < 0) {
+            if (intersect_leaf<ANY, STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, bb1, bb2, prims_tested, found))
+                return true;
+            leaf = node;
+            if (node < 0) {
+                node = st.load(sp);
+                sp--;
+            }
+        }
+    }
+    return found;
+}
+
+template <bool ANY, bool STATS, int W>
+__device__ __forceinline__ bool trace_ray(const DeviceScene &sc, const RayPre &r, float tmin, float &tmax,
+                                          uint32_t &best_key, uint32_t &best_idx, float &bb1, float &bb2, Stack &st,
+                                          uint32_t &nv, uint32_t &pt) {
+    if constexpr (W == 4) return traverse4<ANY, STATS>(sc, r, tmin, tmax, best_key, best_idx, bb1, bb2, st, nv, pt);
+    else return traverse<ANY, STATS>(sc, r, tmin, tmax, best_key, best_idx, bb1, bb2, st, nv, pt);
+}
+
+// counters[0..1]: closest-hit (extend / ray queries), counters[14..15]: shadow
+template <bool STATS>
+__device__ __forceinline__ void flush_stats(const TraceStats *stats, uint32_t nv, uint32_t pt, int base = 0) {
+    if (!STATS) return;
+    // wave reduction then one atomic per wave
+    unsigned long long a = nv, b = pt;
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o);
+        b += __shfl_xor(b, o);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(&stats->counters[base + 0], a);
+        atomicAdd(&stats->counters[base + 1], b);
+    }
+}
+
+
+// ------------------------------------------------------------------ persistent 4-wide traversal
+// The production trace kernels for the quantized BVH4.  Waves are persistent
+// and pull rays from the queue with one atomic per wave; a lane whose ray has
+// terminated is refilled as soon as `refill` lanes of its wave are idle
+// (Aila & Laine 2009, "dynamic fetch"), so a wave never idles on its longest
+// ray.  The stack is a 16-entry LDS ring per lane that spills its oldest 8
+// entries to HBM when full, so push/pop are LDS-only in the common case.
+constexpr int kSpill = 8;
+static_assert((kRing & (kRing - 1)) == 0, "ring size must be a power of two");
+
+struct RingStack {
+    int *lds;  // this lane's column (stride kTraceBlock)
+    int *ovf;  // this lane's overflow column (stride ovf_stride)
+    uint32_t ovf_stride;
+    int sp;   // logical entries [0, sp)
+    int bot;  // entries [0, bot) live in ovf, [bot, sp) in the ring
+
+    __device__ __forceinline__ int &slot(int i) { return lds[(i & (kRing - 1)) * kTraceBlock]; }
+    __device__ __forceinline__ void reset() { sp = bot = 0; }
+    // Make room for three pushes.  The overflow column holds kStackOvf entries;
+    // create() rejects trees needing more than kTraceStackEntries (3 per BVH4
+    // level + 2 per instance entry), so the guard below never triggers.
+    __device__ __forceinline__ void reserve3() {
+        if (sp + 3 - bot > kRing && bot + kSpill <= kStackOvf) {
+#pragma unroll
+            for (int k = 0; k < kSpill; k++) ovf[(uint32_t)(bot + k) * ovf_stride] = slot(bot + k);
+            bot += kSpill;
+        }
+    }
+    __device__ __forceinline__ void push(int v, bool keep) {
+        slot(sp) = v;  // harmless above the top when !keep
+        sp += keep ? 1 : 0;
+    }
+    __device__ __forceinline__ int pop() {
+        if (sp == 0) return kSentinel;
+        sp--;
+        if (sp < bot) {
+            bot -= kSpill;
+#pragma unroll
+            for (int k = 0; k < kSpill; k++) slot(bot + k) = ovf[(uint32_t)(bot + k) * ovf_stride];
+        }
+        return slot(sp);
+    }
+};
+
+// Child order of a BVH4 visit (A/B, PUPIL_SORT at build time): 5 = full sort (the
+// nearest child is descended, the others pushed far to near); 4 = nearest first and
+// farthest pushed first, the middle two unordered; 3 = nearest first only.  Only the
+// traversal order changes: hits are resolved by the (t, id) total order either way.
+#ifndef PUPIL_SORT
+#define PUPIL_SORT 5
+#endif
+
+// Branch-free compare-exchange (selects, no divergent swap blocks).
+__device__ __forceinline__ void csel(float &ta, int &la, float &tb, int &lb) {
+    const bool c = tb < ta;
+    const float t0 = c ? tb : ta, t1 = c ? ta : tb;
+    const int l0 = c ? lb : la, l1 = c ? la : lb;
+    ta = t0;
+    tb = t1;
+    la = l0;
+    lb = l1;
+}
+
+// kModeMixed: one launch over the concatenated next + shadow lists of a bounce
+// (q.nxsh[0, cnt_next) extension rays, then cnt_shadow shadow rays), so each
+// bounce pays one persistent-kernel tail instead of two.
+// kModeMixedAhead: kModeMixed plus the next render's camera rays (render-ahead,
+// TraceJob::ahead_off); a separate instance so the plain mixed kernel keeps its registers
+enum TraceMode : int { kModeExtend = 0, kModeShadow = 1, kModeRays = 2, kModeMixed = 3, kModeMixedAhead = 4 };
+
+struct TraceJob {
+    const uint32_t *queue;      // extend: path ids (null = identity)
+    const uint32_t *count_ptr;  // device count (null = static_count)
+    uint32_t static_count;
+    uint32_t *work;             // kWorkKind counters: heads, final and sub exit counters (stride kWorkStride), zero at launch
+    uint32_t refill;            // refill when at least this many lanes are idle (1..64)
+    uint32_t node_min;          // node phase ends when fewer lanes than this still need a node (>= 1)
+    const float *rays;          // kModeRays: 8 floats per ray (o, d, tmin, tmax)
+    float *out;                 // kModeRays: 4 floats per ray
+    // primary extend (queue == null): list position i -> path (i % spp) * num_local + i / spp,
+    // so consecutive lanes take the spp samples of one pixel (coherent camera rays) while
+    // path ids stay sample major; spp = 0: identity
+    uint32_t spp;
+    uint32_t num_local;
+    // kModeMixedAhead (render-ahead, engine.hip): static_count camera rays of the next render
+    // ride along; the path state passed is the base of both halves of the buffers, list path
+    // ids are offset by list_base (this render's half), ahead position j -> path (pixel-major
+    // as above) + ahead_base (the other half); both offsets are non-negative
+    uint32_t list_base;
+    uint32_t ahead_base;
+};
+
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pk2(float a, float b) {
+    pf2 v;
+    v.x = a;
+    v.y = b;
+    return v;
+}
+__device__ __forceinline__ pf2 splat(float a) { return pk2(a, a); }
+__device__ __forceinline__ pf2 pfma(pf2 a, pf2 b, pf2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ float ubyte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xFFu); }
+
+// One node of the quantized BVH4.  Child plane k on an axis is
+// P = o_node + q_k * s (s a power of two, so q_k * s is exact; the builder
+// verified that fl(P) bounds the child box).  The slab distance is evaluated as
+//     t = fma(q_k, s * idir, (o_node - o_ray) * idir -/+ E)
+// i.e. one fma per plane, with per-node terms shared by the four children.  E
+// bounds every rounding against the exact (fl(P) - o_ray) / d:
+//   |o_node - o_ray| |idir| 5.03u  (subtraction, product, fma, idir rounding)
+// + |o_node| |idir| 1.01u          (fl(P) vs P)
+// + 765 s |idir| 1.01u             (fma rounding of the q*s*idir part, idir rounding)
+// + 1.01u E;  E = (|o_node - o_ray| + |o_node| + 512 s) |idir| 2^-21 covers it
+// (2^-21 = 8u) even after its own rounding.  Near planes are lowered and far
+// planes raised by E, so the test is conservative: a box containing a
+// primitive the exact test would report is never culled, and closest hits stay
+// independent of the BVH.  Overflow (huge idir) gives +-inf/NaN planes, which
+// fmaxf/fminf ignore (IEEE maxNum), i.e. no culling on that axis.
+struct AxisTerms {
+    float b;       // s * idir (exact)
+    float an, af;  // (o_node - o_ray) * idir - E, + E
+};
+
+// PAD (two-level BLAS nodes): the object-space ray carries a position margin
+// `pad` (DevInstance::margin), added to the bound before scaling by |idir|.
+template <bool PAD>
+__device__ __forceinline__ AxisTerms axis_terms(float onode, float s, float oray, float idir, float pad) {
+    AxisTerms t;
+    const float A = onode - oray;
+    const float a = A * idir;
+    const float e = PAD ? __builtin_fmaf(__builtin_fmaf(512.f, s, fabsf(A) + fabsf(onode)), 0x1p-21f, pad) * fabsf(idir)
+                        : __builtin_fmaf(512.f, s, fabsf(A) + fabsf(onode)) * (fabsf(idir) * 0x1p-21f);
+    t.b = s * idir;
+    t.an = a - e;
+    t.af = a + e;
+    return t;
+}
+
+template <bool PAD>
+__device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, float pad, float tmin, float tmax,
+                                       float t[4], int l[4]) {
+    constexpr float kInf = __builtin_huge_valf();
+    const float sx = n.sx, sy = n.sy, sz = n.sz;
+    const bool px = ridir.x >= 0.f, py = ridir.y >= 0.f, pz = ridir.z >= 0.f;
+    const uint32_t nx = px ? n.qlo_x : n.qhi_x, fx = px ? n.qhi_x : n.qlo_x;
+    const uint32_t ny = py ? n.qlo_y : n.qhi_y, fy = py ? n.qhi_y : n.qlo_y;
+    const uint32_t nz = pz ? n.qlo_z : n.qhi_z, fz = pz ? n.qhi_z : n.qlo_z;
+    const AxisTerms X = axis_terms<PAD>(n.ox, sx, ro.x, ridir.x, pad);
+    const AxisTerms Y = axis_terms<PAD>(n.oy, sy, ro.y, ridir.y, pad);
+    const AxisTerms Z = axis_terms<PAD>(n.oz, sz, ro.z, ridir.z, pad);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float tn = fmaxf(fmaxf(fmaxf(__builtin_fmaf(ubyte(nx, k), X.b, X.an), __builtin_fmaf(ubyte(ny, k), Y.b, Y.an)),
+                                     __builtin_fmaf(ubyte(nz, k), Z.b, Z.an)),
+                               tmin);
+        const float tf = fminf(fminf(fminf(__builtin_fmaf(ubyte(fx, k), X.b, X.af), __builtin_fmaf(ubyte(fy, k), Y.b, Y.af)),
+                                     __builtin_fmaf(ubyte(fz, k), Z.b, Z.af)),
+                               tmax);
+        l[k] = n.child[k];
+        t[k] = (tn <= tf && l[k] != kEmptyLink) ? tn : kInf;
+    }
+    csel(t[0], l[0], t[1], l[1]);
+    csel(t[2], l[2], t[3], l[3]);
+    csel(t[0], l[0], t[2], l[2]);
+#if PUPIL_SORT >= 4
+    csel(t[1], l[1], t[3], l[3]);
+#endif
+#if PUPIL_SORT >= 5
+    csel(t[1], l[1], t[2], l[2]);
+#endif
+}
+
+// Node fetch by a 32-bit byte offset from the uniform base (the engine keeps node
+// arrays to at most 2^26 nodes = 4 GiB, kMaxNodes4), which the compiler turns into
+// SGPR-base + VGPR-offset loads: one VALU op per visit instead of a 64-bit shift and add.
+__device__ __forceinline__ Bvh4Node load_node4(const DeviceScene &sc, int node) {
+    return *reinterpret_cast<const Bvh4Node *>(reinterpret_cast<const char *>(sc.nodes4) + ((uint32_t)node << 6));
+}
+
+
+}  // namespace tr
+}  // namespace pupil
