@@ -183,7 +183,7 @@ struct pupil_pt {
         (void)hipFree(p);
     }
     void release_state() {
-        void *bufs[] = {ps.ray_o, ps.ray_d, ps.hit,  ps.thr,  ps.rad,    ps.misc, ps.sh_o,
+        void *bufs[] = {ps.ray_o, ps.ray_d, ps.hit,  ps.thr,  ps.rad,    ps.misc,
                         ps.sh_d, ps.sh_c, ps.mbin, ps.sflags, q.bins, q.nxsh, q.hist};
         for (void *b : bufs)
             if (b) (void)hipFree(b);
@@ -364,7 +364,6 @@ int ensure_state(pupil_pt *pt, size_t paths) {
     HIP_TRY(hipMalloc((void **)&pt->ps.thr, sizeof(float4) * n));
     HIP_TRY(hipMalloc((void **)&pt->ps.rad, sizeof(float4) * n));
     HIP_TRY(hipMalloc((void **)&pt->ps.misc, sizeof(uint4) * n));
-    HIP_TRY(hipMalloc((void **)&pt->ps.sh_o, sizeof(float4) * n));
     HIP_TRY(hipMalloc((void **)&pt->ps.sh_d, sizeof(float4) * n));
     HIP_TRY(hipMalloc((void **)&pt->ps.sh_c, sizeof(float4) * n));
     HIP_TRY(hipMalloc((void **)&pt->ps.mbin, n));
@@ -441,7 +440,7 @@ struct RenderCtx {
         PathState v = pt->ps;
         const size_t o = (size_t)h * paths;
         v.ray_o += o, v.ray_d += o, v.hit += o, v.thr += o, v.rad += o, v.misc += o;
-        v.sh_o += o, v.sh_d += o, v.sh_c += o, v.mbin += o, v.sflags += o;
+        v.sh_d += o, v.sh_c += o, v.mbin += o, v.sflags += o;
         return v;
     }
 };
@@ -536,7 +535,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
     uint32_t K = 1;
     if (may_pipe) {
         K = pt->pipe_limit ? std::min(pt->pipe_limit, D) : D;
-        constexpr double kPathBytes = 9 * 16 + 2 + 4 + 8 + 1;  // PathState + bins + nxsh + partition scratch
+        constexpr double kPathBytes = 8 * 16 + 2 + 4 + 8 + 1;  // PathState + bins + nxsh + partition scratch
         K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::floor(pt->pipe_budget / ((double)np * kPathBytes))));
         while (K > 1 && (uint64_t)K * np >= (1ull << 31)) K--;
     }

@@ -37,13 +37,12 @@ constexpr uint32_t kMissIndex = 0xFFFFFFFFu;
 // Path state in HBM, structure of arrays indexed by path id
 // p = sample * num_local_pixels + local_pixel.
 struct PathState {
-    float4 *ray_o;      // xyz origin of the current ray
+    float4 *ray_o;      // xyz origin of the current ray (and of its shadow ray: w = the shadow ray's tmax)
     float4 *ray_d;      // xyz direction
     float4 *hit;        // t, b1, b2, sorted primitive index (bits) or kMissIndex
     float4 *thr;        // xyz throughput, w = pdf of the BSDF sample that spawned the ray
     float4 *rad;        // xyz radiance
     uint4 *misc;        // x rng, y bounce (bits 0..23) | delta << 31, z/w texcoord (stale semantics, geometry.h:298-304)
-    float4 *sh_o;       // shadow ray origin, w = tmax
     float4 *sh_d;       // shadow ray direction
     float4 *sh_c;       // pending NEE contribution
     uint8_t *mbin;      // extend -> material bin of the hit (0 miss, 1..7 EMatType, 8 unknown), 0xFF = not traced

@@ -159,7 +159,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         tmax = kMaxDistance;
                     } else if (MODE == kModeShadow) {
                         p = shadow_q[i];
-                        o = ps.sh_o[p];
+                        o = ps.ray_o[p];  // shadow rays share the origin record, w = tmax
                         d = ps.sh_d[p];
                         tmin = 0.001f;
                         tmax = o.w;
@@ -176,7 +176,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     } else if (kMixed) {
                         p = q.nxsh[i] + (MODE == kModeMixedAhead ? job.list_base : 0u);
                         any = i >= n_next;
-                        o = any ? ps.sh_o[p] : ps.ray_o[p];
+                        o = ps.ray_o[p];
                         d = any ? ps.sh_d[p] : ps.ray_d[p];
                         tmin = 0.001f;
                         tmax = any ? o.w : kMaxDistance;
@@ -576,7 +576,9 @@ __device__ __forceinline__ const DevEmitter *select_emitter(const DeviceScene &s
 // MIS at the hit, loop head, NEE sample, BSDF sample (main.cu:84-163).
 // Returns the next/shadow flags byte (bit 0 extension ray, bit 1 shadow ray).
 // p: path id (in a pipelined ring: slot * num_paths + sample * num_local + local pixel);
-// misc: its PathState::misc record (bounce in y), already loaded by the launch.
+// its bounce is PathState::misc.y (loaded inside shade_hit / shade_miss: passing the
+// record in from the launch kept it live across the whole shade, 137 instead of 123
+// VGPRs, one wave less per SIMD).
 // Last sample of its frame, and the local pixel (AOVs are written for the last sample).
 __device__ __forceinline__ bool last_sample(const FrameParams &fp, uint32_t p, uint32_t &l) {
     const uint32_t q = p / fp.num_local;
@@ -586,12 +588,13 @@ __device__ __forceinline__ bool last_sample(const FrameParams &fp, uint32_t p, u
 
 template <uint32_t MAT>
 __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
-                                              uint32_t p, uint4 misc) {
+                                              uint32_t p) {
     bool push_next = false, push_shadow = false;
     const float4 h = ps.hit[p];
     const float4 o4 = ps.ray_o[p];
     const float4 d4 = ps.ray_d[p];
     const vec3 ray_o = f3(o4), ray_d = f3(d4);
+    const uint4 misc = ps.misc[p];
     uint32_t rng = misc.x;
     const uint32_t flags = misc.y;
     const uint32_t bounce = flags & 0xFFFFFFu;
@@ -649,7 +652,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         if (rng_next(rng) > rr) alive = false;
         else T = T / rr;
     }
-    float pdf_b = 0.f;
+    float pdf_b = 0.f, sh_tmax = 0.f;
     uint32_t delta = 0;
     const bool nee = alive;  // the reference traces its shadow ray here unconditionally (main.cu:119-123)
     if (alive) {
@@ -673,7 +676,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
                     const float mis = mis_weight(es.pdf, er.pdf);
                     const float pdf_l = es.pdf * sel_prob;
                     const vec3 C = T * es.radiance * er.f * NoL * mis / pdf_l;
-                    ps.sh_o[p] = f4(geo.position, es.distance - 0.001f);
+                    sh_tmax = es.distance - 0.001f;
                     ps.sh_d[p] = f4(es.wi, 0.f);
                     ps.sh_c[p] = f4(C, 0.f);
                     push_shadow = true;
@@ -693,13 +696,15 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         } else {
             T = T * (br.f * fabs_(br.wi.z) / br.pdf);
             const vec3 nd = to_world(br.wi, geo.normal);
-            ps.ray_o[p] = f4(geo.position, 0.f);
             ps.ray_d[p] = f4(nd, 0.f);
             pdf_b = br.pdf;
             delta = (br.sampled_type & kLobeDelta) ? 1u : 0u;
             push_next = true;
         }
     }
+    // the shadow ray starts where the extension ray does (main.cu:119-123,158): one origin
+    // record for both, w = the shadow ray's tmax (the extension ray's tmax is a constant)
+    if (push_shadow || push_next) ps.ray_o[p] = f4(geo.position, sh_tmax);
     ps.thr[p] = f4(T, pdf_b);
     ps.rad[p] = f4(L, 0.f);
     ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
@@ -710,7 +715,8 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
 // Paths whose ray left the scene (__miss__default, main.cu:196-212, and the
 // env handling at main.cu:87-99 / 165-169).
 __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
-                                           uint32_t p, uint4 misc) {
+                                           uint32_t p) {
+    const uint4 misc = ps.misc[p];
     if ((misc.y & 0xFFFFFFu) == 0u) {
         float4 rad4 = ps.rad[p];
         vec3 L = f3(rad4);
@@ -777,18 +783,17 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, Frame
         } else {
             bin = ps.mbin[p];
         }
-        const uint4 misc = ps.misc[p];
         uint32_t flags = 0;
         switch (bin) {
-        case 0: shade_miss(sc, fp, ps, p, misc); break;
-        case PUPIL_MAT_DIFFUSE: flags = shade_hit<PUPIL_MAT_DIFFUSE>(sc, fp, ps, p, misc); break;
-        case PUPIL_MAT_DIELECTRIC: flags = shade_hit<PUPIL_MAT_DIELECTRIC>(sc, fp, ps, p, misc); break;
-        case PUPIL_MAT_ROUGH_DIELECTRIC: flags = shade_hit<PUPIL_MAT_ROUGH_DIELECTRIC>(sc, fp, ps, p, misc); break;
-        case PUPIL_MAT_CONDUCTOR: flags = shade_hit<PUPIL_MAT_CONDUCTOR>(sc, fp, ps, p, misc); break;
-        case PUPIL_MAT_ROUGH_CONDUCTOR: flags = shade_hit<PUPIL_MAT_ROUGH_CONDUCTOR>(sc, fp, ps, p, misc); break;
-        case PUPIL_MAT_PLASTIC: flags = shade_hit<PUPIL_MAT_PLASTIC>(sc, fp, ps, p, misc); break;
-        case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p, misc); break;
-        default: flags = shade_hit<0u>(sc, fp, ps, p, misc); break;
+        case 0: shade_miss(sc, fp, ps, p); break;
+        case PUPIL_MAT_DIFFUSE: flags = shade_hit<PUPIL_MAT_DIFFUSE>(sc, fp, ps, p); break;
+        case PUPIL_MAT_DIELECTRIC: flags = shade_hit<PUPIL_MAT_DIELECTRIC>(sc, fp, ps, p); break;
+        case PUPIL_MAT_ROUGH_DIELECTRIC: flags = shade_hit<PUPIL_MAT_ROUGH_DIELECTRIC>(sc, fp, ps, p); break;
+        case PUPIL_MAT_CONDUCTOR: flags = shade_hit<PUPIL_MAT_CONDUCTOR>(sc, fp, ps, p); break;
+        case PUPIL_MAT_ROUGH_CONDUCTOR: flags = shade_hit<PUPIL_MAT_ROUGH_CONDUCTOR>(sc, fp, ps, p); break;
+        case PUPIL_MAT_PLASTIC: flags = shade_hit<PUPIL_MAT_PLASTIC>(sc, fp, ps, p); break;
+        case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p); break;
+        default: flags = shade_hit<0u>(sc, fp, ps, p); break;
         }
         if (fp.nee_count) {  // collect_stats only: the reference's shadow-ray count, one atomic per wave
             const unsigned long long m = __ballot((flags & 4u) != 0u);

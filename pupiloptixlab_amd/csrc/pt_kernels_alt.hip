@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow(DeviceScene sc, PathStat
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = gtid; i < count; i += stride) {
         const uint32_t p = shadow_q[i];
-        const float4 o = ps.sh_o[p];
+        const float4 o = ps.ray_o[p];  // w = tmax
         const float4 d = ps.sh_d[p];
         const RayPre r = ray_pre(f3(o), f3(d));
         float tmax = o.w;
@@ -271,14 +271,14 @@ __device__ __forceinline__ void trace8_body(const DeviceScene &sc, const PathSta
                         tmax = kMaxDistance;
                     } else if (MODE == kModeShadow) {
                         p = shadow_q[i];
-                        o = ps.sh_o[p];
+                        o = ps.ray_o[p];
                         d = ps.sh_d[p];
                         tmin = 0.001f;
                         tmax = o.w;
                     } else if (MODE == kModeMixed) {
                         p = q.nxsh[i];
                         any = i >= n_next;
-                        o = any ? ps.sh_o[p] : ps.ray_o[p];
+                        o = ps.ray_o[p];
                         d = any ? ps.sh_d[p] : ps.ray_d[p];
                         tmin = 0.001f;
                         tmax = any ? o.w : kMaxDistance;
