@@ -369,9 +369,9 @@ def pmc_record(args):
 
 def gather_ceiling(footprint_bytes):
     """Dependent random 64-B gather ceiling of this GPU (G fetches/s), measured now by
-    build/ubench_gather on a table of the next power of two above the traversal's
-    footprint (BVH nodes + primitive records), so the ceiling is not overstated by a
-    table that caches better than the real arrays."""
+    build/ubench_gather on a table of the next power of two at or above the node array
+    (the fetches the node-gather figure counts), so the ceiling is not overstated by a
+    table smaller than the real array."""
     import subprocess
 
     exe = os.path.join(HERE, "build", "ubench_gather")
@@ -402,15 +402,15 @@ def roofline(args, st_bytes, timed):
     kernel = ("k_trace4 (persistent BVH4 traversal; pipelined frames: one launch per step over the shadow + "
               "extension rays of every frame in flight and the newest frame's camera rays)")
     cands = {}
-    footprint = 64.0 * st_bytes["bvh_nodes"] + 48.0 * st_bytes["bvh_prims"]
+    footprint = 64.0 * st_bytes["bvh_nodes"]
     ceil = gather_ceiling(footprint)
     if ceil and sec > 0:
         cands["node-gather"] = {"achieved": nodes / sec / 1e9, "peak": ceil["ceiling_gnodes_per_s"],
                                 "unit": "Gnode/s",
                                 "how": "distinct node fetches per ray (counter frame) x rays per launch / HIP-event "
-                                       "launch time; peak = build/ubench_gather dependent random 64-B gathers on a "
-                                       f"{ceil['table_mb']:.0f} MB table (>= the BVH nodes + primitive records, "
-                                       f"{footprint / 1e6:.0f} MB), best waves/SIMD, measured in this run",
+                                       "launch time; peak = build/ubench_gather dependent uniformly random 64-B gathers "
+                                       f"on a {ceil['table_mb']:.0f} MB table (>= the {footprint / 1e6:.0f} MB node array), "
+                                       "best waves/SIMD, measured in this run",
                                 "node_visits_per_launch": round(visits, 1),
                                 "distinct_fetches_per_launch": round(nodes, 1),
                                 "ceiling_per_waves_per_simd": ceil.get("per_waves_per_simd")}
@@ -432,6 +432,14 @@ def roofline(args, st_bytes, timed):
     for c in cands.values():
         c["frac"] = round(c["achieved"] / c["peak"], 4)
         c["achieved"] = round(c["achieved"], 2)
+    # a rate above the uniform-random gather rate is no ceiling: the traversal's fetches
+    # have locality (hot upper levels in L2, coherent waves) that random gathers lack
+    # (config 5's 137 MB node array); such a figure is reported but cannot bind
+    binding = {k: v for k, v in cands.items() if v["frac"] <= 1.0}
+    for k, v in cands.items():
+        if v["frac"] > 1.0:
+            v["note"] = ("above the uniform-random gather rate of a node-array-sized table: the traversal's fetches "
+                         "are served with more locality than random gathers; not a ceiling")
     out = {"kernel": kernel, "ms_per_launch": round(ms, 4), "launches": int(launches),
            "rays_per_launch": round(rays_launch, 1), "traffic": round(traffic, 1) if traffic else None,
            # SURVEY.md §8(d) algorithmic bytes (32 B ray + 16 B hit + 64 B/node + 48 B/primitive): the BVH
@@ -439,8 +447,8 @@ def roofline(args, st_bytes, timed):
            "algorithmic": {"bytes_per_launch": round(alg_bytes, 1),
                            "gbs": round(alg_bytes / sec / 1e9, 1) if sec > 0 else None},
            "ceilings": cands}
-    if cands:
-        bound = max(cands, key=lambda k: cands[k]["frac"])
+    if binding:
+        bound = max(binding, key=lambda k: binding[k]["frac"])
         b = cands[bound]
         out.update({"bound": bound, "achieved": b["achieved"], "peak": round(b["peak"], 2), "unit": b["unit"],
                     "frac": b["frac"]})

@@ -117,7 +117,7 @@ struct pupil_pt {
     uint32_t pipe_run = 0;            // consecutive renders that continued the previous one
     uint32_t pipe_gen = 0;            // iterations so far (flags tags)
     uint32_t pipe_limit = 0;          // PUPIL_PIPE: most slots (0 = max_depth)
-    double pipe_budget = 96e9;        // PUPIL_PIPE_GB: most HBM bytes for the ring's path state
+    double pipe_budget = 160e9;       // PUPIL_PIPE_GB: most HBM bytes for the ring's path state (of 288 GB)
     bool pipe_valid = false;          // cleared by camera / instance / emitter updates
     float *aov_scratch = nullptr;     // K slots x 7 floats per local pixel
     size_t aov_cap = 0;

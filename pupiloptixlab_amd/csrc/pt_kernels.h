@@ -11,7 +11,10 @@
 namespace pupil {
 
 constexpr int kTraceBlock = 128;
-constexpr int kTraceWavesPerSimd = 7;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8: 2 % slower)
+#ifndef PUPIL_W4_WAVES  // A/B builds only
+#define PUPIL_W4_WAVES 7
+#endif
+constexpr int kTraceWavesPerSimd = PUPIL_W4_WAVES;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8 waves at <= 64 VGPRs: 11 % slower, r03 A/B)
 #ifndef PUPIL_W8_WAVES  // A/B builds only (tools/dbg: the spilled 6-wave BVH8 kernels)
 #define PUPIL_W8_WAVES 5
 #endif

@@ -48,8 +48,21 @@ def test_roofline_one_gpu_per_launch_and_binding_ceiling(monkeypatch):
     assert r["bound"] == max(c, key=lambda k: c[k]["frac"])
     assert r["frac"] == c[r["bound"]]["frac"]
     assert list(r)[:6] == ["bound", "achieved", "peak", "unit", "frac", "traffic"]
-    # the gather ceiling is measured on a table no smaller than nodes + records
-    assert seen["footprint"] == 64.0 * 212619 + 48.0 * 1000014
+    # the gather ceiling is measured on a table no smaller than the node array
+    assert seen["footprint"] == 64.0 * 212619
+
+
+def test_roofline_rate_above_the_gather_table_is_not_a_ceiling(monkeypatch):
+    """config 5: the traversal fetches its 137 MB node array faster than uniformly random
+    gathers on a table of that size -- reported with a note, never chosen as the bound."""
+    _patch(monkeypatch)
+    monkeypatch.setattr(bench, "gather_ceiling", lambda footprint: {
+        "ceiling_gnodes_per_s": 30.0, "table_mb": 268.4, "per_waves_per_simd": {"7": 30.0}})
+    timed = {"trace_ms": 70.0, "launches": 5, "rays": 5 * 98.4e6}
+    r = bench.roofline(A, ST, timed)
+    c = r["ceilings"]
+    assert c["node-gather"]["frac"] > 1 and "note" in c["node-gather"]
+    assert r["bound"] != "node-gather" and r["frac"] <= 1
 
 
 def test_roofline_rank_of_an_8_way_shard_stays_below_one(monkeypatch):
