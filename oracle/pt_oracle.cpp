@@ -1174,6 +1174,7 @@ struct Scene {
     std::vector<QNode> q4;
     std::vector<uint32_t> q4_rec_prim;  // record -> primitive id (the record's a.w)
     int32_t q4_root = kQDone;
+    float q4_bound[3] = {0.f, 0.f, 0.f};  // per axis max |o| + 512 s over q4 (engine node_bound)
     mat4x4 sample_to_camera{}, camera_to_world{};
     std::vector<Material> materials;
     std::vector<Instance> instances;
@@ -1272,21 +1273,20 @@ struct Scene {
     }
 
     // Child entry distances of an engine BVH4 node: the GPU's conservative
-    // quantized slab test restated (pt_kernels.hip visit4 / axis_terms): per axis
-    // t = fma(q, s * idir, (o_node - o_ray) * idir -/+ E),
-    // E = fma(512, s, |o_node - o_ray| + |o_node|) * (|idir| * 2^-21).
-    static void QVisit(const QNode &n, const Ray &r, float tmin, float tmax, float t[4]) {
+    // quantized slab test restated (pt_traverse.h visit4 / slab_error): per axis
+    // t = fma(q, s * idir, fma(o_node - o_ray, idir, -/+E)),
+    // E = (|o_ray| + M) * (|idir| * 2^-21), M = q4_bound (max |o| + 512 s over the nodes).
+    void QVisit(const QNode &n, const Ray &r, float tmin, float tmax, float t[4]) const {
         const float o[3] = {n.ox, n.oy, n.oz}, ro[3] = {r.o.x, r.o.y, r.o.z}, id[3] = {r.idir.x, r.idir.y, r.idir.z};
         float bn[3], an[3], af[3];
         uint32_t qn[3], qf[3];
         for (int a = 0; a < 3; a++) {
             const float sc = a == 0 ? n.sx : (a == 1 ? n.sy : n.sz);
             const float A = o[a] - ro[a];
-            const float av = A * id[a];
-            const float e = std::fma(512.f, sc, std::fabs(A) + std::fabs(o[a])) * (std::fabs(id[a]) * 0x1p-21f);
+            const float e = (std::fabs(ro[a]) + q4_bound[a]) * (std::fabs(id[a]) * 0x1p-21f);
             bn[a] = sc * id[a];
-            an[a] = av - e;
-            af[a] = av + e;
+            an[a] = std::fma(A, id[a], -e);
+            af[a] = std::fma(A, id[a], e);
             const bool pos = id[a] >= 0.f;
             qn[a] = pos ? n.qlo[a] : n.qhi[a];
             qf[a] = pos ? n.qhi[a] : n.qlo[a];
@@ -1717,6 +1717,12 @@ int oracle_set_bvh4(oracle_scene *s, uint32_t num_nodes, const void *nodes, uint
         sc.q4_rec_prim[i] = bits;
     }
     sc.q4_root = root_link;
+    sc.q4_bound[0] = sc.q4_bound[1] = sc.q4_bound[2] = 0.f;
+    for (const auto &n : sc.q4) {
+        sc.q4_bound[0] = std::fmax(sc.q4_bound[0], std::fabs(n.ox) + 512.f * n.sx);
+        sc.q4_bound[1] = std::fmax(sc.q4_bound[1], std::fabs(n.oy) + 512.f * n.sy);
+        sc.q4_bound[2] = std::fmax(sc.q4_bound[2], std::fabs(n.oz) + 512.f * n.sz);
+    }
     for (const auto &n : sc.q4)
         for (int k = 0; k < 4; k++)
             if (n.child[k] >= 0 && n.child[k] != oracle::kQEmpty && (uint32_t)n.child[k] >= num_nodes) return -1;

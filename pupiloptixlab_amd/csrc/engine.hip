@@ -139,6 +139,7 @@ struct pupil_pt {
     uint32_t *ray_log = nullptr;                   // per iteration of the last render: next, shadow
     uint32_t ray_log_cap = 0;                      // iterations it holds
     unsigned long long *ray_cum = nullptr;         // device running totals: next, shadow rays
+    uint32_t *node_bound = nullptr;                // launch_node_bound's result (3 floats as bits)
     uint64_t primary_cum = 0;                      // host running total of camera rays
     uint32_t last_paths = 0, last_iters = 0;
     uint64_t last_primary = 0;
@@ -376,12 +377,27 @@ int ensure_state(pupil_pt *pt, size_t paths) {
     return PUPIL_OK;
 }
 
-// Local pixel list of a rank: tiles t with t % world == rank, row-major tile
-// order, row-major pixels inside a tile (clipped at the image border).
 // BVH4 node array the traversal walks (its size bounds the 32-bit node offsets, kMaxNodes4)
 uint64_t nodes4_count(const pupil_pt *pt) {
     return pt->two_level ? (pt->tl.world ? pt->tl.num_wnodes : pt->tl.num_nodes4) : pt->bvh.num_nodes4;
 }
+
+// DeviceScene::node_bound of the current BVH4 arrays (after every build and refit;
+// one 12-B read back, the traversal kernels take it by value)
+int refresh_node_bound(pupil_pt *pt) {
+    pt->sc.node_bound[0] = pt->sc.node_bound[1] = pt->sc.node_bound[2] = 0.f;
+    const uint64_t n = nodes4_count(pt);
+    if (pt->sc.bvh_width != 4 || !pt->sc.nodes4 || n == 0) return PUPIL_OK;
+    launch_node_bound(pt->sc.nodes4, n, pt->node_bound, pt->own_stream);
+    uint32_t b[3];
+    HIP_TRY(hipMemcpyAsync(b, pt->node_bound, sizeof(b), hipMemcpyDeviceToHost, pt->own_stream));
+    HIP_TRY(hipStreamSynchronize(pt->own_stream));
+    for (int a = 0; a < 3; a++) std::memcpy(&pt->sc.node_bound[a], &b[a], 4);
+    return PUPIL_OK;
+}
+
+// Local pixel list of a rank: tiles t with t % world == rank, row-major tile
+// order, row-major pixels inside a tile (clipped at the image border).
 
 uint32_t local_pixels(uint32_t w, uint32_t h, uint32_t ts, uint32_t rank, uint32_t world, uint32_t *out) {
     if (world <= 1) {
@@ -907,7 +923,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     // traversal overflow stacks, counters, events
     pt->ovf_threads = trace_grid_blocks() * (uint32_t)kTraceBlock;
     if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 32) ||
-        pt->alloc(&pt->ray_cum, 2) || pt->alloc(&pt->q.counts, kCountSlots) ||
+        pt->alloc(&pt->ray_cum, 2) || pt->alloc(&pt->node_bound, 3) || pt->alloc(&pt->q.counts, kCountSlots) ||
         pt->alloc(&pt->q.work, kWorkSlots))
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
     if (hipMemset(pt->q.work, 0, kWorkSlots * sizeof(uint32_t)) != hipSuccess ||
@@ -915,6 +931,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         return cleanup(fail(PUPIL_ERR_HIP, "workspace clear failed"));
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
+    if (refresh_node_bound(pt) != PUPIL_OK) return cleanup(PUPIL_ERR_HIP);
     pt->totals.bvh_nodes = pt->two_level ? two_level_nodes(pt->tl)
                            : (pt->sc.bvh_width == 8 ? pt->bvh.num_nodes8
                                                     : (pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes));
@@ -961,6 +978,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
         if (trc == -3) return fail(PUPIL_ERR_UNSUPPORTED, "TLAS + BLAS deeper than the traversal stacks hold");
         if (trc != 0) return fail(PUPIL_ERR_HIP, "TLAS rebuild failed");
         pt->sc.root_link4 = pt->tl.root_link4;
+        if (const int rc = refresh_node_bound(pt)) return rc;
         pt->totals.bvh_nodes = two_level_nodes(pt->tl);
         pt->totals.bvh_depth = pt->tl.tlas_depth + pt->tl.blas_depth;
         pt->totals.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -974,7 +992,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
         double rms = 0.0;
         if (refit_bvh4(bin, pt->bvh, instance, pt->own_stream, &rms) == 0) {
             pt->totals.build_ms = rms;
-            return PUPIL_OK;
+            return refresh_node_bound(pt);
         }
     }
     BvhBuildOutput nb{};
@@ -998,7 +1016,7 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     pt->totals.bvh_nodes = pt->sc.bvh_width == 8 ? nb.num_nodes8 : (pt->sc.bvh_width == 4 ? nb.num_nodes4 : nb.num_nodes);
     pt->totals.bvh_depth = pt->sc.bvh_width == 8 ? nb.depth8 : nb.depth4;
     pt->totals.build_ms = ms;
-    return PUPIL_OK;
+    return refresh_node_bound(pt);
 }
 
 // EmitterHelper reset after a transform change (world/world.cpp:45-54): the area

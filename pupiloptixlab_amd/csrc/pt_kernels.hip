@@ -32,9 +32,10 @@ namespace {
 using namespace tr;
 
 // Two-level: the object-space box ray of instance `in` (origin, reciprocal
-// direction) and its position margin at the exit of the instance's world box.
-__device__ __forceinline__ void enter_instance(const DevInstance &in, const RayPre &r, float tmax, vec3 &bo, vec3 &bi,
-                                               float &pad) {
+// direction) and its slab-test bound (pt_traverse.h slab_error_pad), which adds the
+// position margin at the exit of the instance's world box.
+__device__ __forceinline__ void enter_instance(const DevInstance &in, const RayPre &r, float tmax, const float bound[3],
+                                               vec3 &bo, vec3 &bi, vec3 &be) {
     bo = xform_point(in.to_object, r.o);
     const vec3 d = xform_vector(in.to_object, r.d);
     const float tiny = 1e-30f;
@@ -47,7 +48,9 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
     te = fabsf(te) * 1.0001f;
     const float on = fmaxf(fmaxf(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z));
     const float dn = fmaxf(fmaxf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
-    pad = __builtin_fmaf(in.margin[0], __builtin_fmaf(te, dn, on), in.margin[1]);
+    const float pad = __builtin_fmaf(in.margin[0], __builtin_fmaf(te, dn, on), in.margin[1]);
+    be = v3(slab_error_pad(bo.x, bi.x, bound[0], pad), slab_error_pad(bo.y, bi.y, bound[1], pad),
+            slab_error_pad(bo.z, bi.z, bound[2], pad));
 }
 
 // TL = two-level acceleration (DeviceScene::two_level): the TLAS leaves hold one
@@ -102,7 +105,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     bool in_blas = false;  // TL: traversing an instance's BLAS
     uint32_t inst = 0;
     vec3 bo = v3(0.f), bi = v3(0.f);  // TL: box-test ray (object space inside a BLAS)
-    float bpad = 0.f;
+    vec3 be = v3(0.f);                // its slab-test bound (pt_traverse.h slab_error)
     for (;;) {
         // ---- refill idle lanes (one atomic per wave)
         const unsigned long long idle = __ballot(!active);
@@ -196,11 +199,11 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     st.reset();
                     node = (int)sc.root_link4;
                     leaf = 0;
+                    be = slab_errors(r.o, r.idir, sc.node_bound);
                     if (TL) {
                         in_blas = false;
                         bo = r.o;
                         bi = r.idir;
-                        bpad = 0.f;
                     }
                     if (node < 0) {
                         leaf = node;
@@ -238,8 +241,8 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 }
                 float t[4];
                 int l[4];
-                if (TL) visit4<true>(n, bo, bi, bpad, tmin, tmax, t, l);
-                else visit4<false>(n, r.o, r.idir, 0.f, tmin, tmax, t, l);
+                if (TL) visit4(n, bo, bi, be, tmin, tmax, t, l);
+                else visit4(n, r.o, r.idir, be, tmin, tmax, t, l);
                 if (t[0] == kInf) {
                     node = st.pop();
                 } else {
@@ -289,7 +292,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         st.push(kReturnLink, true);
                         in_blas = true;
                         inst = id;
-                        enter_instance(in, r, tmax, bo, bi, bpad);
+                        enter_instance(in, r, tmax, sc.node_bound, bo, bi, be);
                         node = in.blas_root;
                         leaf = 0;
                         if (node < 0) {
@@ -313,7 +316,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 in_blas = false;
                 bo = r.o;
                 bi = r.idir;
-                bpad = 0.f;
+                be = slab_errors(r.o, r.idir, sc.node_bound);
                 node = st.pop();
                 if (node < 0) {
                     leaf = node;
@@ -986,6 +989,27 @@ void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState 
     default: SHADE(kShadeBins); break;
     }
 #undef SHADE
+}
+
+__global__ __launch_bounds__(256) void k_node_bound(const Bvh4Node *nodes, uint64_t n, uint32_t *out) {
+    float m[3] = {0.f, 0.f, 0.f};
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull) {
+        const Bvh4Node &b = nodes[i];
+        m[0] = fmaxf(m[0], fabsf(b.ox) + 512.f * b.sx);  // upward rounding: slack of slab_error
+        m[1] = fmaxf(m[1], fabsf(b.oy) + 512.f * b.sy);
+        m[2] = fmaxf(m[2], fabsf(b.oz) + 512.f * b.sz);
+    }
+    for (int a = 0; a < 3; a++) {
+        float v = m[a];
+        for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+        if (lane_id() == 0) atomicMax(out + a, __float_as_uint(v));  // non-negative: uint order
+    }
+}
+
+void launch_node_bound(const Bvh4Node *nodes, uint64_t n, uint32_t *out, hipStream_t s) {
+    (void)hipMemsetAsync(out, 0, 3 * sizeof(uint32_t), s);
+    const uint64_t blocks = std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + 255) / 256));
+    hipLaunchKernelGGL(k_node_bound, dim3((uint32_t)blocks), dim3(256), 0, s, nodes, n, out);
 }
 
 void launch_accumulate(const FrameParams &fp, const PathState &ps, const float *aov_src, bool clear_flags,

@@ -159,6 +159,24 @@ __device__ __forceinline__ uint32_t xor_permute8(uint32_t m, uint32_t oct) {
     return m ^ (t | (t << 4));
 }
 
+// BVH8 (A/B family): the per-node rounding bound of r02 (pt_traverse.h visit4 takes
+// one per ray from DeviceScene::node_bound, which the engine computes for BVH4 only):
+// E = fma(512, s, |o_node - o_ray| + |o_node|) * |idir| 2^-21 for this node's o and s
+struct AxisTerms {
+    float b;       // s * idir (exact)
+    float an, af;  // (o_node - o_ray) * idir - E, + E
+};
+__device__ __forceinline__ AxisTerms axis_terms8(float onode, float s, float oray, float idir) {
+    AxisTerms t;
+    const float A = onode - oray;
+    const float a = A * idir;
+    const float e = __builtin_fmaf(512.f, s, fabsf(A) + fabsf(onode)) * (fabsf(idir) * 0x1p-21f);
+    t.b = s * idir;
+    t.an = a - e;
+    t.af = a + e;
+    return t;
+}
+
 // The eight child boxes of a Bvh8Node with visit4's conservative slab test.
 // Returns the node-group word of the hit internal children (priority order) and
 // the record-slot bits of the hit leaf children.
@@ -175,9 +193,9 @@ __device__ __forceinline__ void visit8(const uint4 w0, const uint4 w2, const uin
     const uint32_t nx0 = px ? w2.x : w2.z, nx1 = px ? w2.y : w2.w, fx0 = px ? w2.z : w2.x, fx1 = px ? w2.w : w2.y;
     const uint32_t ny0 = py ? w3.x : w3.z, ny1 = py ? w3.y : w3.w, fy0 = py ? w3.z : w3.x, fy1 = py ? w3.w : w3.y;
     const uint32_t nz0 = pz ? w4.x : w4.z, nz1 = pz ? w4.y : w4.w, fz0 = pz ? w4.z : w4.x, fz1 = pz ? w4.w : w4.y;
-    const AxisTerms X = axis_terms<false>(ox, sx, ro.x, ridir.x, 0.f);
-    const AxisTerms Y = axis_terms<false>(oy, sy, ro.y, ridir.y, 0.f);
-    const AxisTerms Z = axis_terms<false>(oz, sz, ro.z, ridir.z, 0.f);
+    const AxisTerms X = axis_terms8(ox, sx, ro.x, ridir.x);
+    const AxisTerms Y = axis_terms8(oy, sy, ro.y, ridir.y);
+    const AxisTerms Z = axis_terms8(oz, sz, ro.z, ridir.z);
     uint32_t acc = 0u;
 #pragma unroll
     for (int k = 0; k < 8; k++) {

@@ -169,6 +169,10 @@ struct DeviceScene {
     uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
     uint32_t num_cus;       // compute units of the device (persistent grid size)
     uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node
+    // per axis, max over every BVH4 node of |o| + 512 s (launch_node_bound after each build
+    // and refit): the slab test's rounding bound is then one value per ray (pt_traverse.h
+    // slab_error) instead of one per node visit
+    float node_bound[3];
     // every instance has this material bin (1..8; 0 = several): shading then derives a
     // path's bin from its hit record and the persistent traversal writes no bin byte
     uint32_t single_bin;

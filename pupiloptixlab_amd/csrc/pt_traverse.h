@@ -426,71 +426,56 @@ struct TraceJob {
     uint32_t ahead_base;
 };
 
-typedef float pf2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ pf2 pk2(float a, float b) {
-    pf2 v;
-    v.x = a;
-    v.y = b;
-    return v;
-}
-__device__ __forceinline__ pf2 splat(float a) { return pk2(a, a); }
-__device__ __forceinline__ pf2 pfma(pf2 a, pf2 b, pf2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ float ubyte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xFFu); }
 
 // One node of the quantized BVH4.  Child plane k on an axis is
 // P = o_node + q_k * s (s a power of two, so q_k * s is exact; the builder
 // verified that fl(P) bounds the child box).  The slab distance is evaluated as
-//     t = fma(q_k, s * idir, (o_node - o_ray) * idir -/+ E)
-// i.e. one fma per plane, with per-node terms shared by the four children.  E
-// bounds every rounding against the exact (fl(P) - o_ray) / d:
-//   |o_node - o_ray| |idir| 5.03u  (subtraction, product, fma, idir rounding)
-// + |o_node| |idir| 1.01u          (fl(P) vs P)
-// + 765 s |idir| 1.01u             (fma rounding of the q*s*idir part, idir rounding)
-// + 1.01u E;  E = (|o_node - o_ray| + |o_node| + 512 s) |idir| 2^-21 covers it
-// (2^-21 = 8u) even after its own rounding.  Near planes are lowered and far
-// planes raised by E, so the test is conservative: a box containing a
-// primitive the exact test would report is never culled, and closest hits stay
-// independent of the BVH.  Overflow (huge idir) gives +-inf/NaN planes, which
-// fmaxf/fminf ignore (IEEE maxNum), i.e. no culling on that axis.
-struct AxisTerms {
-    float b;       // s * idir (exact)
-    float an, af;  // (o_node - o_ray) * idir - E, + E
-};
-
-// PAD (two-level BLAS nodes): the object-space ray carries a position margin
-// `pad` (DevInstance::margin), added to the bound before scaling by |idir|.
-template <bool PAD>
-__device__ __forceinline__ AxisTerms axis_terms(float onode, float s, float oray, float idir, float pad) {
-    AxisTerms t;
-    const float A = onode - oray;
-    const float a = A * idir;
-    const float e = PAD ? __builtin_fmaf(__builtin_fmaf(512.f, s, fabsf(A) + fabsf(onode)), 0x1p-21f, pad) * fabsf(idir)
-                        : __builtin_fmaf(512.f, s, fabsf(A) + fabsf(onode)) * (fabsf(idir) * 0x1p-21f);
-    t.b = s * idir;
-    t.an = a - e;
-    t.af = a + e;
-    return t;
+//     t = fma(q_k, s * idir, fma(o_node - o_ray, idir, -/+E))
+// i.e. one fma per plane and three operations per axis and node shared by the four
+// children.  E bounds every rounding against the exact (fl(P) - o_ray) / d
+// (u = 2^-24; subtraction, both fmas, idir, fl(P) vs P):
+//   u |idir| (5 |o_node| + 4 |o_ray| + 765 s) + 2u E
+// and is taken per RAY, not per node: with M >= |o_node| + 512 s over every node
+// (DeviceScene::node_bound, launch_node_bound)
+//   E = (|o_ray| + M) |idir| 2^-21   (2^-21 = 8u)
+// covers it with room for its own two roundings.  Near planes are lowered and far
+// planes raised by E, so the test is conservative: a box containing a primitive the
+// exact test would report is never culled, and closest hits stay independent of the
+// BVH.  Overflow (huge idir) gives +-inf/NaN planes, which fmaxf/fminf ignore (IEEE
+// maxNum), i.e. no culling on that axis.  (r02/r03 evaluated E per node from that
+// node's o and s: 7 operations per axis instead of 3.)
+__device__ __forceinline__ float slab_error(float oray, float idir, float bound) {
+    return (fabsf(oray) + bound) * (fabsf(idir) * 0x1p-21f);
+}
+// two-level BLAS nodes: the object-space ray carries a position margin `pad`
+// (DevInstance::margin), added to the bound before scaling by |idir|
+__device__ __forceinline__ float slab_error_pad(float oray, float idir, float bound, float pad) {
+    return __builtin_fmaf(fabsf(oray) + bound, 0x1p-21f, pad) * fabsf(idir);
+}
+__device__ __forceinline__ vec3 slab_errors(vec3 o, vec3 idir, const float bound[3]) {
+    return v3(slab_error(o.x, idir.x, bound[0]), slab_error(o.y, idir.y, bound[1]), slab_error(o.z, idir.z, bound[2]));
 }
 
-template <bool PAD>
-__device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, float pad, float tmin, float tmax,
+__device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, vec3 e, float tmin, float tmax,
                                        float t[4], int l[4]) {
     constexpr float kInf = __builtin_huge_valf();
-    const float sx = n.sx, sy = n.sy, sz = n.sz;
     const bool px = ridir.x >= 0.f, py = ridir.y >= 0.f, pz = ridir.z >= 0.f;
     const uint32_t nx = px ? n.qlo_x : n.qhi_x, fx = px ? n.qhi_x : n.qlo_x;
     const uint32_t ny = py ? n.qlo_y : n.qhi_y, fy = py ? n.qhi_y : n.qlo_y;
     const uint32_t nz = pz ? n.qlo_z : n.qhi_z, fz = pz ? n.qhi_z : n.qlo_z;
-    const AxisTerms X = axis_terms<PAD>(n.ox, sx, ro.x, ridir.x, pad);
-    const AxisTerms Y = axis_terms<PAD>(n.oy, sy, ro.y, ridir.y, pad);
-    const AxisTerms Z = axis_terms<PAD>(n.oz, sz, ro.z, ridir.z, pad);
+    const float ax = n.ox - ro.x, ay = n.oy - ro.y, az = n.oz - ro.z;
+    const float bx = n.sx * ridir.x, by = n.sy * ridir.y, bz = n.sz * ridir.z;
+    const float nearx = __builtin_fmaf(ax, ridir.x, -e.x), farx = __builtin_fmaf(ax, ridir.x, e.x);
+    const float neary = __builtin_fmaf(ay, ridir.y, -e.y), fary = __builtin_fmaf(ay, ridir.y, e.y);
+    const float nearz = __builtin_fmaf(az, ridir.z, -e.z), farz = __builtin_fmaf(az, ridir.z, e.z);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const float tn = fmaxf(fmaxf(fmaxf(__builtin_fmaf(ubyte(nx, k), X.b, X.an), __builtin_fmaf(ubyte(ny, k), Y.b, Y.an)),
-                                     __builtin_fmaf(ubyte(nz, k), Z.b, Z.an)),
+        const float tn = fmaxf(fmaxf(fmaxf(__builtin_fmaf(ubyte(nx, k), bx, nearx), __builtin_fmaf(ubyte(ny, k), by, neary)),
+                                     __builtin_fmaf(ubyte(nz, k), bz, nearz)),
                                tmin);
-        const float tf = fminf(fminf(fminf(__builtin_fmaf(ubyte(fx, k), X.b, X.af), __builtin_fmaf(ubyte(fy, k), Y.b, Y.af)),
-                                     __builtin_fmaf(ubyte(fz, k), Z.b, Z.af)),
+        const float tf = fminf(fminf(fminf(__builtin_fmaf(ubyte(fx, k), bx, farx), __builtin_fmaf(ubyte(fy, k), by, fary)),
+                                     __builtin_fmaf(ubyte(fz, k), bz, farz)),
                                tmax);
         l[k] = n.child[k];
         t[k] = (tn <= tf && l[k] != kEmptyLink) ? tn : kInf;

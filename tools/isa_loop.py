@@ -62,10 +62,11 @@ def main(obj, kernel, out_path=None):
         open(out_path, "w").write("\n".join(lines) + "\n")
     body = [l for l in lines if not l.startswith("<")]
     print(f"{kernel}: {len(body)} instructions", dict(Counter(klass(l) for l in body)))
-    # node loop: from the first block with 4 consecutive global_load_dwordx4 (the node) to the
+    # node loop: from the first block with 4 global_load_dwordx4 within 5 lines (the node) to the
     # first ds_write after it (the stack pushes) and the loop-control tail up to the back-edge
-    idx = next(i for i in range(len(lines) - 3)
-               if all(lines[i + k].startswith("global_load_dwordx4") for k in range(4)))
+    idx = next(i for i in range(len(lines) - 4)
+               if sum(lines[i + k].startswith("global_load_dwordx4") for k in range(5)) == 4
+               and lines[i].startswith("global_load_dwordx4"))
     start = max(j for j in range(idx) if lines[j].startswith("<"))
     seg = []
     for l in lines[start:]:
