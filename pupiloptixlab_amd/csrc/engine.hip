@@ -118,6 +118,12 @@ struct pupil_pt {
     uint32_t pipe_gen = 0;            // iterations so far (flags tags)
     uint32_t pipe_limit = 0;          // PUPIL_PIPE: most slots (0 = max_depth)
     double pipe_budget = 160e9;       // PUPIL_PIPE_GB: most HBM bytes for the ring's path state (of 288 GB)
+    // PUPIL_PIPE_PATHS: a ring needs no more slots than it takes to put this many paths in
+    // flight.  Frames ahead pay off by filling the launch tails of small launches; past
+    // ~64 M paths per launch the tail is amortised and a larger ring only spreads the
+    // traversal's path-state accesses (config 5, 133 M paths per frame: 2288 Mrays/s with
+    // one slot, 2208 / 2195 / 2155 / 2093 with 2 / 3 / 4 / 6, profiles/r03_pipe_sweep_config5.txt)
+    double pipe_paths = 64e6;
     bool pipe_valid = false;          // cleared by camera / instance / emitter updates
     float *aov_scratch = nullptr;     // K slots x 7 floats per local pixel
     size_t aov_cap = 0;
@@ -553,6 +559,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         K = pt->pipe_limit ? std::min(pt->pipe_limit, D) : D;
         constexpr double kPathBytes = 8 * 16 + 2 + 4 + 8 + 1;  // PathState + bins + nxsh + partition scratch
         K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::floor(pt->pipe_budget / ((double)np * kPathBytes))));
+        K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::ceil(pt->pipe_paths / (double)np)));
         while (K > 1 && (uint64_t)K * np >= (1ull << 31)) K--;
     }
     const uint32_t key[8] = {cx.key[0], cx.key[1], cx.key[2], cx.key[3], cx.key[4], fp.spp, D, fp.num_local};
@@ -911,6 +918,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (const char *a = std::getenv("PUPIL_AHEAD")) pt->ahead_mode = std::min(2, std::max(0, std::atoi(a)));
     if (const char *k = std::getenv("PUPIL_PIPE")) pt->pipe_limit = (uint32_t)std::min(63, std::max(0, std::atoi(k)));
     if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
+    if (const char *g = std::getenv("PUPIL_PIPE_PATHS")) pt->pipe_paths = std::max(1.0, std::atof(g));
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     if (sc.bvh_width == 4 && nodes4_count(pt) > kMaxNodes4)
