@@ -133,7 +133,9 @@ def main():
         # the engine pipeline frames (engine.hip render_pipelined: the step's one traversal
         # launch also advances the frames of the next steps).  collect_stats=4: HIP events
         # around the traversal launches only, summed over the timed steps
-        pt.render(args.spp, stream=stream, continues=True, collect_stats=4)
+        split = int(os.environ.get("PUPIL_BENCH_SPLIT", "1"))  # A/B: the step's spp as `split` renders
+        for _ in range(split):
+            pt.render(args.spp // split, stream=stream, continues=True, collect_stats=4)
         if gather is not None:  # overlapped with the next frame on a side stream (dist.FrameGather)
             handles.append(gather.gather_async(pt.buffers.get(FINAL_RESULT), stream))
 
