@@ -207,8 +207,10 @@ struct HostBox {
     }
 };
 
-// Top-down SAH split of ids[b, e) (centroid sort on the widest axis, sweep).
-// binned (or null): counts the splits the binned SAH chose
+// Top-down SAH split of ids[b, e) over all three axes (r02 tried the widest centroid
+// axis only): ranges above 1024 entries (world-mode braided entries) by 64-bin binned
+// SAH per axis, O(n) per split; smaller ones by a full sweep over the centroid order
+// of each axis.  binned (or null): counts the splits the binned SAH chose.
 uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std::vector<HostBox> &boxes,
                    uint32_t *binned) {
     HostBox cb = HostBox::empty();
@@ -220,23 +222,22 @@ uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std
             cb.hi[k] = std::max(cb.hi[k], c);
         }
     }
-    int axis = 0;
-    for (int k = 1; k < 3; k++)
-        if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
-    if (e - b > 1024) {  // large ranges (world-mode braided entries): binned SAH, O(n) per split
+    const uint32_t n = e - b;
+    if (n > 1024) {
         constexpr int kBins = 64;
-        const float lo = cb.lo[axis], ext = cb.hi[axis] - cb.lo[axis];
-        if (ext > 0.f) {
+        float best = __builtin_huge_valf();
+        int best_axis = -1, best_cut = 0;
+        for (int axis = 0; axis < 3; axis++) {
+            const float lo = cb.lo[axis], ext = cb.hi[axis] - cb.lo[axis];
+            if (!(ext > 0.f)) continue;
             HostBox bb[kBins];
             uint32_t cnt[kBins] = {};
             for (auto &x : bb) x = HostBox::empty();
-            auto bin_of = [&](uint32_t id) {
-                const float c = 0.5f * (boxes[id].lo[axis] + boxes[id].hi[axis]);
-                return std::min(kBins - 1, std::max(0, (int)((c - lo) / ext * kBins)));
-            };
             for (uint32_t i = b; i < e; i++) {
-                const int k = bin_of(ids[i]);
-                bb[k].grow(boxes[ids[i]]);
+                const HostBox &x = boxes[ids[i]];
+                const float c = 0.5f * (x.lo[axis] + x.hi[axis]);
+                const int k = std::min(kBins - 1, std::max(0, (int)((c - lo) / ext * kBins)));
+                bb[k].grow(x);
                 cnt[k]++;
             }
             float right[kBins];
@@ -249,20 +250,24 @@ uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std
             }
             acc = HostBox::empty();
             uint32_t ln = 0;
-            float best = __builtin_huge_valf();
-            int cut = kBins / 2;
             for (int k = 1; k < kBins; k++) {
                 acc.grow(bb[k - 1]);
                 ln += cnt[k - 1];
-                if (ln == 0 || ln == e - b) continue;
+                if (ln == 0 || ln == n) continue;
                 const float cost = acc.area() * (float)ln + right[k];
                 if (cost < best) {
                     best = cost;
-                    cut = k;
+                    best_axis = axis;
+                    best_cut = k;
                 }
             }
-            const auto mid = std::stable_partition(ids.begin() + b, ids.begin() + e,
-                                                   [&](uint32_t id) { return bin_of(id) < cut; });
+        }
+        if (best_axis >= 0) {
+            const float lo = cb.lo[best_axis], ext = cb.hi[best_axis] - cb.lo[best_axis];
+            const auto mid = std::stable_partition(ids.begin() + b, ids.begin() + e, [&](uint32_t id) {
+                const float c = 0.5f * (boxes[id].lo[best_axis] + boxes[id].hi[best_axis]);
+                return std::min(kBins - 1, std::max(0, (int)((c - lo) / ext * kBins))) < best_cut;
+            });
             const uint32_t m = (uint32_t)(mid - ids.begin());
             if (m > b && m < e) {
                 if (binned) (*binned)++;
@@ -270,28 +275,36 @@ uint32_t sah_split(std::vector<uint32_t> &ids, uint32_t b, uint32_t e, const std
             }
         }
     }
-    std::stable_sort(ids.begin() + b, ids.begin() + e, [&](uint32_t x, uint32_t y) {
-        return boxes[x].lo[axis] + boxes[x].hi[axis] < boxes[y].lo[axis] + boxes[y].hi[axis];
-    });
-    const uint32_t n = e - b;
-    std::vector<float> right(n + 1, 0.f);
-    HostBox acc = HostBox::empty();
-    for (uint32_t i = n; i-- > 1;) {
-        acc.grow(boxes[ids[b + i]]);
-        right[i] = acc.area() * (float)(n - i);
-    }
-    acc = HostBox::empty();
+    // full sweep per axis over the centroid order; the best axis's order is kept
     float best = __builtin_huge_valf();
-    uint32_t split = b + n / 2;
-    for (uint32_t i = 1; i < n; i++) {
-        acc.grow(boxes[ids[b + i - 1]]);
-        const float cost = acc.area() * (float)i + right[i];
-        if (cost < best) {
-            best = cost;
-            split = b + i;
+    int best_axis = 0;
+    uint32_t best_split = b + n / 2;
+    std::vector<float> right(n + 1, 0.f);
+    for (int axis = 0; axis < 3; axis++) {
+        if (!(cb.hi[axis] - cb.lo[axis] > 0.f) && axis != 2) continue;
+        std::stable_sort(ids.begin() + b, ids.begin() + e, [&](uint32_t x, uint32_t y) {
+            return boxes[x].lo[axis] + boxes[x].hi[axis] < boxes[y].lo[axis] + boxes[y].hi[axis];
+        });
+        HostBox acc = HostBox::empty();
+        for (uint32_t i = n; i-- > 1;) {
+            acc.grow(boxes[ids[b + i]]);
+            right[i] = acc.area() * (float)(n - i);
+        }
+        acc = HostBox::empty();
+        for (uint32_t i = 1; i < n; i++) {
+            acc.grow(boxes[ids[b + i - 1]]);
+            const float cost = acc.area() * (float)i + right[i];
+            if (cost < best) {
+                best = cost;
+                best_axis = axis;
+                best_split = b + i;
+            }
         }
     }
-    return split;
+    std::stable_sort(ids.begin() + b, ids.begin() + e, [&](uint32_t x, uint32_t y) {
+        return boxes[x].lo[best_axis] + boxes[x].hi[best_axis] < boxes[y].lo[best_axis] + boxes[y].hi[best_axis];
+    });
+    return best_split;
 }
 
 // 4-wide TLAS node over ids[b, e) (two levels of binary SAH splits); returns its link.
