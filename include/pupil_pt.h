@@ -268,8 +268,9 @@ typedef struct pupil_pt_counters {
     /* frames started ahead of the next render (pipelined frames) and the ring size */
     uint64_t frames_in_flight;
     uint64_t pipeline_slots;
-    /* two-level structure: TLAS nodes whose children were chosen by the binned SAH (an
-     * entry range too large for the exact split search, accel_two_level.hip) */
+    /* two-level structure: TLAS nodes placed by an SAH at the last TLAS build -- every node
+     * of a GPU-built TLAS (world mode above 64 entries: PLOC + SAH-optimal collapse), or the
+     * host builder's binned-SAH splits (entry ranges above 1024, accel_two_level.hip) */
     uint64_t tlas_sah_splits;
     /* collect_stats, persistent traversal kernels: list items the dequeue heads handed
      * out, lanes activated with them, lanes retired, and the launches' list lengths --

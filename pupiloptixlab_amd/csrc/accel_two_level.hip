@@ -436,10 +436,8 @@ void refresh_instance_margins(DevInstance &d) {
 // ias_manager.cpp:116-151).  TLAS nodes are numbered parent first, so walking them
 // backwards sees every child before its parent.
 bool refit_world_tlas(TwoLevelAccel &acc, uint32_t n, hipStream_t s) {
-    if (acc.tlas_host.size() != acc.tlas_nodes || acc.tlas_nodes == 0) return false;
-    std::unordered_map<int, std::array<float, 6>> eb;
-    for (uint32_t i = 0; i < n; i++)
-        for (const auto &e : acc.entries[i]) eb[e.first] = e.second;
+    if (acc.tlas_host.size() != acc.tlas_nodes || acc.tlas_nodes == 0 || acc.tlas_eref.size() != 4ull * acc.tlas_nodes)
+        return false;
     std::vector<std::array<float, 6>> nb(acc.tlas_nodes);
     for (uint32_t v = acc.tlas_nodes; v-- > 0;) {
         Bvh4Node &nd = acc.tlas_host[v];
@@ -454,9 +452,10 @@ bool refit_world_tlas(TwoLevelAccel &acc, uint32_t n, hipStream_t s) {
             if (l >= 0 && (uint32_t)l < acc.tlas_nodes) {
                 b = nb[(size_t)l];
             } else {
-                auto it = eb.find(l);
-                if (it == eb.end()) return false;
-                b = it->second;
+                const auto &r = acc.tlas_eref[4 * (size_t)v + k];
+                if (r.first >= n || r.second >= acc.entries[r.first].size() || acc.entries[r.first][r.second].first != l)
+                    return false;  // not the entry the TLAS was built over: rebuild
+                b = acc.entries[r.first][r.second].second;
             }
             for (int a = 0; a < 3; a++) {
                 clo[a][nk] = b[a];
@@ -537,8 +536,45 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
         uint32_t depth = 0;
         int root = kTraverseDone;
         uint32_t binned = 0;
-        if (ids.size() == 1) root = links[0];
-        else if (!ids.empty()) root = build_tlas_node(ids, 0, (uint32_t)ids.size(), eb, nodes, 0u, depth, &links, &binned);
+        // above 64 entries the TLAS is built like the flattened BVH (GPU Morton order, PLOC,
+        // SAH-optimal 4-wide collapse, one entry per leaf) and its leaf links are replaced by
+        // the entries' links; PUPIL_TL_BUILDER=host keeps the host's top-down binned SAH
+        const char *tb = std::getenv("PUPIL_TL_BUILDER");
+        const bool gpu_tlas = ids.size() > 64 && !(tb && std::strcmp(tb, "host") == 0);
+        if (ids.size() == 1) {
+            root = links[0];
+        } else if (gpu_tlas) {
+            std::vector<uint32_t> order;
+            if (build_bvh4_over_boxes(&eb[0].lo[0], (uint32_t)eb.size(), nodes, order, &depth, s) != 0) return -1;
+            // PUPIL_TL_ORDER=dfs (A/B): TLAS nodes renumbered in preorder (still parents first)
+            const char *to = std::getenv("PUPIL_TL_ORDER");
+            if (to && std::strcmp(to, "dfs") == 0 && nodes.size() > 1) {
+                std::vector<uint32_t> nid(nodes.size(), 0xFFFFFFFFu), stack{0u};
+                uint32_t next = 0;
+                while (!stack.empty()) {
+                    const uint32_t v = stack.back();
+                    stack.pop_back();
+                    nid[v] = next++;
+                    for (int k = 3; k >= 0; k--)
+                        if (nodes[v].child[k] >= 0 && nodes[v].child[k] != kEmptyLink) stack.push_back((uint32_t)nodes[v].child[k]);
+                }
+                std::vector<Bvh4Node> o(nodes.size());
+                for (size_t v = 0; v < nodes.size(); v++) {
+                    Bvh4Node nd = nodes[v];
+                    for (int k = 0; k < 4; k++)
+                        if (nd.child[k] >= 0 && nd.child[k] != kEmptyLink) nd.child[k] = (int)nid[nd.child[k]];
+                    o[nid[v]] = nd;
+                }
+                nodes.swap(o);
+            }
+            for (Bvh4Node &nd : nodes)
+                for (int k = 0; k < 4; k++)
+                    if (nd.child[k] < 0) nd.child[k] = links[order[leaf_first(nd.child[k])]];
+            root = 0;
+            binned = (uint32_t)nodes.size();  // every TLAS node placed by the SAH collapse
+        } else if (!ids.empty()) {
+            root = build_tlas_node(ids, 0, (uint32_t)ids.size(), eb, nodes, 0u, depth, &links, &binned);
+        }
         if (nodes.size() > acc.tlas_cap) return -1;
         if (3u * depth + 3u * acc.blas_depth > (uint32_t)kTraceStackEntries) return -3;
         acc.tlas_depth = depth;
@@ -549,6 +585,19 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
         acc.tlas_nodes = (uint32_t)nodes.size();
         acc.sah_splits = binned;
         acc.tlas_host = nodes;
+        {  // entry slots of the TLAS for its refits (one lookup table per build)
+            std::unordered_map<int, std::pair<uint32_t, uint32_t>> where;
+            for (uint32_t i = 0; i < n; i++)
+                for (uint32_t j = 0; j < (uint32_t)acc.entries[i].size(); j++) where[acc.entries[i][j].first] = {i, j};
+            acc.tlas_eref.assign(4 * nodes.size(), {~0u, 0u});
+            for (size_t v = 0; v < nodes.size(); v++)
+                for (int k = 0; k < 4; k++) {
+                    const int l = nodes[v].child[k];
+                    if (l == kEmptyLink || (l >= 0 && (uint32_t)l < nodes.size())) continue;
+                    const auto it = where.find(l);
+                    if (it != where.end()) acc.tlas_eref[4 * v + k] = it->second;
+                }
+        }
         acc.root_link4 = (uint32_t)root;
         return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
     }
@@ -587,9 +636,10 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     const uint32_t n = (uint32_t)insts.size();
     const char *mode = std::getenv("PUPIL_TL_MODE");  // world (default) | object (A/B)
     acc.world = !(mode && std::strcmp(mode, "object") == 0);
-    // braid 5 = TLAS over the nodes 5 levels below each instance root (config 5, r02: braid 0 / 3 / 4 / 5 / 6 ->
-    // 1557 / 1766 / 1918 / 2026 / 2052 Mrays/s vs 2205 flattened; deeper only lengthens the TLAS build)
-    if (const char *b = std::getenv("PUPIL_TL_BRAID")) acc.braid = (uint32_t)std::min(6, std::max(0, std::atoi(b)));
+    // braid 6 = TLAS over the nodes 6 levels below each instance root.  Config 5 with the GPU-built
+    // TLAS (r03, profiles/r03_tlas_gpu_ab.txt): braid 5 / 6 / 7 / 8 -> 461 / 443 / 451 / 423 ms per step,
+    // instance update 7 / 26 / 134-171 / 830 ms (the host refit of the TLAS grows with its entries)
+    if (const char *b = std::getenv("PUPIL_TL_BRAID")) acc.braid = (uint32_t)std::min(8, std::max(0, std::atoi(b)));
     // BLAS per mesh shape that some instance uses
     std::vector<uint8_t> used(shapes.size(), 0);
     std::vector<uint32_t> shape_of(n);

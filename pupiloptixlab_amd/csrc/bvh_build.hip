@@ -1481,6 +1481,75 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     return err == hipSuccess ? 0 : -2;
 }
 
+// BVH4 over n boxes (lo xyz, hi xyz; the world-mode TLAS over braided entries,
+// accel_two_level.hip): Morton order, PLOC and the SAH-optimal collapse of the flattened
+// build with one box per leaf.  On return `nodes` holds the 4-wide nodes (root 0,
+// breadth first: parents before children) whose leaf links make_leaf(p, 1) name the
+// box order[p].  n >= 2.
+int build_bvh4_over_boxes(const float *h_boxes, uint32_t n, std::vector<Bvh4Node> &nodes, std::vector<uint32_t> &order,
+                          uint32_t *depth, hipStream_t s) {
+    if (n < 2) return -1;
+    const int m = (int)n;
+    Aabb *boxes = nullptr, *node_boxes = nullptr;
+    uint32_t *bounds = nullptr, *keys = nullptr, *vals = nullptr, *keys2 = nullptr, *vals2 = nullptr, *hist = nullptr;
+    int2 *children = nullptr, *ranges = nullptr;
+    int *parent_internal = nullptr, *parent_leaf = nullptr;
+    Bvh4Node *nodes4 = nullptr;
+    const uint32_t nblocks = (n + kSortTile - 1) / kSortTile;
+    hipError_t err = dmalloc(&boxes, n);
+    if (!err) err = dmalloc(&node_boxes, n);
+    if (!err) err = dmalloc(&bounds, 6);
+    if (!err) err = dmalloc(&keys, n);
+    if (!err) err = dmalloc(&vals, n);
+    if (!err) err = dmalloc(&keys2, n);
+    if (!err) err = dmalloc(&vals2, n);
+    if (!err) err = dmalloc(&hist, 256 * (size_t)nblocks);
+    if (!err) err = dmalloc(&children, n);
+    if (!err) err = dmalloc(&ranges, n);
+    if (!err) err = dmalloc(&parent_internal, n);
+    if (!err) err = dmalloc(&parent_leaf, n);
+    if (!err) err = dmalloc(&nodes4, n - 1);
+    uint32_t num4 = 0, d4 = 0;
+    uint32_t *vi = vals, *vo = vals2;
+    if (!err) err = hipMemcpyAsync(boxes, h_boxes, sizeof(Aabb) * n, hipMemcpyHostToDevice, s);
+    if (!err) {
+        const uint32_t g = (n + kBlock - 1) / kBlock;
+        const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+        (void)hipMemcpyAsync(bounds, init, sizeof(init), hipMemcpyHostToDevice, s);
+        hipLaunchKernelGGL(k_bounds, dim3(min(g, 1024u)), dim3(kBlock), 0, s, boxes, n, bounds);
+        hipLaunchKernelGGL(k_morton, dim3(g), dim3(kBlock), 0, s, boxes, n, bounds, keys, vals);
+        uint32_t *ki = keys, *ko = keys2;
+        for (int shift = 0; shift < 30; shift += 8) {
+            hipLaunchKernelGGL(k_sort_hist, dim3(nblocks), dim3(kBlock), 0, s, ki, n, shift, hist, nblocks);
+            hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist, 256u * nblocks);
+            hipLaunchKernelGGL(k_sort_scatter, dim3(nblocks), dim3(kBlock), 0, s, ki, vi, ko, vo, n, shift, hist,
+                               nblocks);
+            std::swap(ki, ko);
+            std::swap(vi, vo);
+        }
+        (void)hipMemsetAsync(parent_internal, 0xFF, sizeof(int) * n, s);
+        err = build_ploc(m, vi, vo, boxes, children, ranges, node_boxes, parent_internal, parent_leaf, s);
+        std::swap(vi, vo);  // vi: the PLOC box order
+        std::vector<uint32_t> level_start;
+        if (!err)
+            err = collapse_bvh4(m, vi, boxes, children, ranges, node_boxes, 1u, nodes4, &num4, &d4, &level_start, s,
+                                true);
+    }
+    if (!err) {
+        nodes.resize(num4);
+        order.resize(n);
+        err = hipMemcpyAsync(nodes.data(), nodes4, sizeof(Bvh4Node) * num4, hipMemcpyDeviceToHost, s);
+        if (!err) err = hipMemcpyAsync(order.data(), vi, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s);
+        if (!err) err = hipStreamSynchronize(s);
+    }
+    if (depth) *depth = d4;
+    for (void *p : {(void *)boxes, (void *)node_boxes, (void *)bounds, (void *)keys, (void *)vals, (void *)keys2,
+                    (void *)vals2, (void *)hist, (void *)children, (void *)ranges, (void *)parent_internal,
+                    (void *)parent_leaf, (void *)nodes4})
+        if (p) (void)hipFree(p);
+    return err == hipSuccess ? 0 : -2;
+}
+
 int build_bvh_bounded(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s,
                       double *build_ms, uint32_t reserve) {
     const auto fits = [&](const BvhBuildOutput &o) {

@@ -216,5 +216,10 @@ void free_lbvh(BvhBuildOutput &out);
 // world vertices and every BVH4 node box is refitted bottom up (topology kept, like the
 // reference's IAS update).  Needs the breadth-first level order; -1 when unavailable.
 int refit_bvh4(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t moved, hipStream_t s, double *ms);
+// BVH4 over n >= 2 boxes (6 floats each: lo xyz, hi xyz) with the flattened build's PLOC +
+// SAH collapse, one box per leaf: nodes (root 0, parents first) and, for leaf link
+// make_leaf(p, 1), the box order[p]; depth = 4-wide levels
+int build_bvh4_over_boxes(const float *h_boxes, uint32_t n, std::vector<Bvh4Node> &nodes,
+                          std::vector<uint32_t> &order, uint32_t *depth, hipStream_t s);
 
 }  // namespace pupil

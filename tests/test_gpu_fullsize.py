@@ -92,5 +92,5 @@ def test_config5_instanced_10m(accel, monkeypatch):
     desc = scenes.instanced_field(40, 3840, 2160, 6, seed=2, spheres_per_blas=125).desc()
     st = check_sample(desc, 16, 97, f"config5-{accel}", offset=11)
     assert st["two_level"] == (accel == "two_level")
-    if accel == "two_level":  # ~40 x 1024 braided TLAS entries: the binned-SAH split ran
+    if accel == "two_level":  # ~40 x 1024 braided TLAS entries: the GPU SAH-collapse TLAS build ran
         assert st["tlas_sah_splits"] > 0, st["tlas_sah_splits"]
