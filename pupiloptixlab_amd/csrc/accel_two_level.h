@@ -36,17 +36,16 @@ struct TwoLevelAccel {
     // structure is one BVH4 the flat traversal kernels walk (no ray transform, no
     // return markers, the flat kernel's occupancy).  HBM pays one BLAS copy per instance.
     bool world = false;
-    uint32_t braid = 6;  // PUPIL_TL_BRAID
+    uint32_t braid = 8;  // PUPIL_TL_BRAID
     Bvh4Node *wnodes = nullptr;  // [0, tlas_cap) TLAS, then the per-instance world BLAS copies
     float *d_wbox = nullptr;     // world box of every copied node (6 floats)
     uint32_t num_wnodes = 0;
     std::vector<std::vector<std::pair<int, std::array<float, 6>>>> entries;  // per instance: TLAS entries
     std::vector<uint32_t> inst_shape;                  // shape of each instance (0xFFFFFFFF: sphere)
-    std::vector<Bvh4Node> tlas_host;                   // host copy of the world-mode TLAS (refits)
-    // per TLAS child slot (4 per node): (instance, position in entries[instance]) of the
-    // braided entry it links, or (~0u, 0) for a TLAS node / empty slot -- refits read the
-    // entries' new boxes without a lookup
-    std::vector<std::pair<uint32_t, uint32_t>> tlas_eref;
+    // world-mode TLAS refits (GPU, one launch per level, deepest first): the TLAS node ids
+    // ordered by level from the deepest (d_tlas_order) and where each level starts in it
+    uint32_t *d_tlas_order = nullptr;
+    std::vector<uint32_t> tlas_level_start;
     std::vector<std::vector<uint32_t>> shape_levels;   // per shape: BVH4 level starts of its BLAS (+ end)
     uint32_t root_link4 = (uint32_t)kTraverseDone;
     double build_ms = 0.0;

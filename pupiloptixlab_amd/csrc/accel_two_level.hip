@@ -24,7 +24,6 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
-#include <unordered_map>
 #include <vector>
 
 #include "accel_two_level.h"
@@ -176,6 +175,73 @@ __global__ __launch_bounds__(kBlock) void k_world_refit(const DevInstance *insts
         for (int a = 0; a < 3; a++) {
             b[a] = nlo[a];
             b[3 + a] = nhi[a];
+        }
+    }
+}
+
+// World-mode TLAS refit (RenderInstanceUpdate; the reference refits its IAS,
+// ias_manager.cpp:116-151): the TLAS keeps its topology and every node over the
+// TLAS level [lo, hi) of `order` gets its child boxes anew -- a TLAS or world BLAS
+// node child: the exact world box its refit left in wbox (TLAS levels run deepest
+// first); a record leaf: the exact bounds of its world records; a sphere record: its
+// instance's world box -- then is quantised conservatively, like k_world_refit.
+__global__ __launch_bounds__(kBlock) void k_tlas_refit(const uint32_t *order, uint32_t lo, uint32_t hi,
+                                                       const float4 *wrec, const float *inst_box, Bvh4Node *wn,
+                                                       float *wbox) {
+    for (uint32_t j = lo + blockIdx.x * blockDim.x + threadIdx.x; j < hi; j += gridDim.x * blockDim.x) {
+        const uint32_t v = order[j];
+        const Bvh4Node n = wn[v];
+        float clo[3][4], chi[3][4], nlo[3], nhi[3];
+        int link[4];
+        int nk = 0;
+        for (int a = 0; a < 3; a++) {
+            nlo[a] = __builtin_huge_valf();
+            nhi[a] = -__builtin_huge_valf();
+        }
+        for (int k = 0; k < 4; k++) {
+            const int l = n.child[k];
+            if (l == kEmptyLink) continue;
+            float bl[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+            float bh[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+            if (l >= 0) {
+                for (int a = 0; a < 3; a++) {
+                    bl[a] = wbox[6 * (size_t)l + a];
+                    bh[a] = wbox[6 * (size_t)l + 3 + a];
+                }
+            } else {
+                const uint32_t first = leaf_first(l), cnt = leaf_count(l);
+                if (__float_as_uint(wrec[3 * (size_t)first].w) & kPrimSphereBit) {
+                    const uint32_t i = __float_as_uint(wrec[3 * (size_t)first + 1].w);
+                    for (int a = 0; a < 3; a++) {
+                        bl[a] = inst_box[6 * (size_t)i + a];
+                        bh[a] = inst_box[6 * (size_t)i + 3 + a];
+                    }
+                } else {
+                    for (uint32_t r = first; r < first + cnt; r++)
+                        for (int c = 0; c < 3; c++) {
+                            const float4 q = wrec[3 * (size_t)r + c];
+                            bl[0] = fminf(bl[0], q.x);
+                            bl[1] = fminf(bl[1], q.y);
+                            bl[2] = fminf(bl[2], q.z);
+                            bh[0] = fmaxf(bh[0], q.x);
+                            bh[1] = fmaxf(bh[1], q.y);
+                            bh[2] = fmaxf(bh[2], q.z);
+                        }
+                }
+            }
+            link[nk] = l;
+            for (int a = 0; a < 3; a++) {
+                clo[a][nk] = bl[a];
+                chi[a][nk] = bh[a];
+                nlo[a] = fminf(nlo[a], bl[a]);
+                nhi[a] = fmaxf(nhi[a], bh[a]);
+            }
+            nk++;
+        }
+        wn[v] = encode_bvh4(nlo, nhi, clo, chi, link, nk);
+        for (int a = 0; a < 3; a++) {
+            wbox[6 * (size_t)v + a] = nlo[a];
+            wbox[6 * (size_t)v + 3 + a] = nhi[a];
         }
     }
 }
@@ -432,45 +498,19 @@ void refresh_instance_margins(DevInstance &d) {
 }
 
 // World mode, RenderInstanceUpdate: the TLAS keeps its topology and its boxes are
-// refitted bottom up to the changed entries (the reference refits its IAS,
-// ias_manager.cpp:116-151).  TLAS nodes are numbered parent first, so walking them
-// backwards sees every child before its parent.
-bool refit_world_tlas(TwoLevelAccel &acc, uint32_t n, hipStream_t s) {
-    if (acc.tlas_host.size() != acc.tlas_nodes || acc.tlas_nodes == 0 || acc.tlas_eref.size() != 4ull * acc.tlas_nodes)
-        return false;
-    std::vector<std::array<float, 6>> nb(acc.tlas_nodes);
-    for (uint32_t v = acc.tlas_nodes; v-- > 0;) {
-        Bvh4Node &nd = acc.tlas_host[v];
-        float clo[3][4], chi[3][4], nlo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()},
-                                    nhi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
-        int link[4];
-        int nk = 0;
-        for (int k = 0; k < 4; k++) {
-            const int l = nd.child[k];
-            if (l == kEmptyLink) continue;
-            std::array<float, 6> b;
-            if (l >= 0 && (uint32_t)l < acc.tlas_nodes) {
-                b = nb[(size_t)l];
-            } else {
-                const auto &r = acc.tlas_eref[4 * (size_t)v + k];
-                if (r.first >= n || r.second >= acc.entries[r.first].size() || acc.entries[r.first][r.second].first != l)
-                    return false;  // not the entry the TLAS was built over: rebuild
-                b = acc.entries[r.first][r.second].second;
-            }
-            for (int a = 0; a < 3; a++) {
-                clo[a][nk] = b[a];
-                chi[a][nk] = b[3 + a];
-                nlo[a] = std::min(nlo[a], b[a]);
-                nhi[a] = std::max(nhi[a], b[3 + a]);
-            }
-            link[nk++] = l;
-        }
-        nd = encode_bvh4(nlo, nhi, clo, chi, link, nk);
-        nb[v] = {nlo[0], nlo[1], nlo[2], nhi[0], nhi[1], nhi[2]};
+// refitted bottom up on the GPU, one launch per TLAS level from the deepest (r03; the
+// host refit it replaces re-encoded every node on the CPU: 26 ms at braid 6, 0.8 s at
+// braid 8).  false: no level order (no TLAS nodes, or a failed build) -- rebuild.
+bool refit_world_tlas(TwoLevelAccel &acc, hipStream_t s) {
+    if (acc.tlas_nodes == 0 || acc.tlas_level_start.size() < 2 || !acc.d_tlas_order) return false;
+    for (size_t L = 0; L + 1 < acc.tlas_level_start.size(); L++) {
+        const uint32_t lo = acc.tlas_level_start[L], hi = acc.tlas_level_start[L + 1];
+        if (hi <= lo) continue;
+        const uint32_t g = std::min(1024u, (hi - lo + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(k_tlas_refit, dim3(std::max(1u, g)), dim3(kBlock), 0, s, acc.d_tlas_order, lo, hi,
+                           acc.wprims, acc.d_boxes, acc.wnodes, acc.d_wbox);
     }
-    return hipMemcpyAsync(acc.wnodes, acc.tlas_host.data(), sizeof(Bvh4Node) * acc.tlas_nodes, hipMemcpyHostToDevice,
-                          s) == hipSuccess &&
-           hipStreamSynchronize(s) == hipSuccess;
+    return hipGetLastError() == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
 }
 
 int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstance *d_insts,
@@ -517,7 +557,7 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
             if (insts[i].kind == PUPIL_SHAPE_SPHERE) sphere_rec[i] = srec++;
         for (uint32_t id : changed)
             if (!world_entries(acc, insts[id], id, sphere_rec[id], s)) return -1;
-        if (refit && refit_world_tlas(acc, n, s)) return 0;
+        if (refit && refit_world_tlas(acc, s)) return 0;
         std::vector<HostBox> eb;
         std::vector<int> links;
         for (uint32_t i = 0; i < n; i++)
@@ -584,19 +624,31 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
             return -1;
         acc.tlas_nodes = (uint32_t)nodes.size();
         acc.sah_splits = binned;
-        acc.tlas_host = nodes;
-        {  // entry slots of the TLAS for its refits (one lookup table per build)
-            std::unordered_map<int, std::pair<uint32_t, uint32_t>> where;
-            for (uint32_t i = 0; i < n; i++)
-                for (uint32_t j = 0; j < (uint32_t)acc.entries[i].size(); j++) where[acc.entries[i][j].first] = {i, j};
-            acc.tlas_eref.assign(4 * nodes.size(), {~0u, 0u});
-            for (size_t v = 0; v < nodes.size(); v++)
+        {  // TLAS levels for the GPU refits: node ids by level, deepest first
+            std::vector<uint32_t> level(nodes.size(), 0u), bfs;
+            if (!nodes.empty()) bfs.push_back(0u);
+            for (size_t h = 0; h < bfs.size(); h++)
                 for (int k = 0; k < 4; k++) {
-                    const int l = nodes[v].child[k];
-                    if (l == kEmptyLink || (l >= 0 && (uint32_t)l < nodes.size())) continue;
-                    const auto it = where.find(l);
-                    if (it != where.end()) acc.tlas_eref[4 * v + k] = it->second;
+                    const int l = nodes[bfs[h]].child[k];
+                    if (l == kEmptyLink || l < 0 || (size_t)l >= nodes.size()) continue;
+                    level[l] = level[bfs[h]] + 1u;
+                    bfs.push_back((uint32_t)l);
                 }
+            acc.tlas_level_start.assign(1, 0u);
+            std::vector<uint32_t> order;
+            if (bfs.size() == nodes.size()) {  // every node reached from the root (node 0)
+                // breadth-first order has non-decreasing levels: reversed, deepest level first
+                order.assign(bfs.rbegin(), bfs.rend());
+                for (uint32_t j = 1; j <= (uint32_t)order.size(); j++)
+                    if (j == (uint32_t)order.size() || level[order[j]] != level[order[j - 1]])
+                        acc.tlas_level_start.push_back(j);
+            } else {
+                acc.tlas_level_start.clear();  // not a tree rooted at node 0: refits rebuild
+            }
+            if (!order.empty() && (hipMemcpyAsync(acc.d_tlas_order, order.data(), sizeof(uint32_t) * order.size(),
+                                                  hipMemcpyHostToDevice, s) != hipSuccess ||
+                                   hipStreamSynchronize(s) != hipSuccess))  // `order` dies with this block
+                return -1;
         }
         acc.root_link4 = (uint32_t)root;
         return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
@@ -636,9 +688,9 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     const uint32_t n = (uint32_t)insts.size();
     const char *mode = std::getenv("PUPIL_TL_MODE");  // world (default) | object (A/B)
     acc.world = !(mode && std::strcmp(mode, "object") == 0);
-    // braid 6 = TLAS over the nodes 6 levels below each instance root.  Config 5 with the GPU-built
-    // TLAS (r03, profiles/r03_tlas_gpu_ab.txt): braid 5 / 6 / 7 / 8 -> 461 / 443 / 451 / 423 ms per step,
-    // instance update 7 / 26 / 134-171 / 830 ms (the host refit of the TLAS grows with its entries)
+    // braid 8 = TLAS over the nodes 8 levels below each instance root.  Config 5 with the GPU-built
+    // TLAS and GPU refits (r03, profiles/r03_tlas_braid_ab.txt): braid 6 / 7 / 8 -> 434 / 445 / 415 ms
+    // per step, instance update 1.4 / 1.5 / 1.9 ms, build 37 / 61 / 131-148 ms
     if (const char *b = std::getenv("PUPIL_TL_BRAID")) acc.braid = (uint32_t)std::min(8, std::max(0, std::atoi(b)));
     // BLAS per mesh shape that some instance uses
     std::vector<uint8_t> used(shapes.size(), 0);
@@ -792,6 +844,7 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         if (wnodes >= (1ull << 31) ||
             hipMalloc((void **)&acc.wnodes, sizeof(Bvh4Node) * (size_t)wnodes) != hipSuccess ||
             hipMalloc((void **)&acc.d_wbox, sizeof(float) * 6 * (size_t)wnodes) != hipSuccess ||
+            hipMalloc((void **)&acc.d_tlas_order, sizeof(uint32_t) * (size_t)std::max(1u, acc.tlas_cap)) != hipSuccess ||
             hipMalloc((void **)&grown, sizeof(float4) * 3 * (size_t)std::max<uint64_t>(1, wbase + spheres)) != hipSuccess ||
             (spheres && hipMemcpy(grown + 3 * wbase, sph.data(), sizeof(float4) * sph.size(), hipMemcpyHostToDevice) !=
                             hipSuccess)) {
@@ -815,7 +868,7 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
 
 void free_two_level(TwoLevelAccel &acc) {
     void *p[] = {acc.nodes4, acc.prims, acc.attrs, acc.d_boxes, acc.d_list, acc.d_verts, acc.wprims, acc.d_faces,
-                 acc.wnodes, acc.d_wbox};
+                 acc.wnodes, acc.d_wbox, acc.d_tlas_order};
     for (void *x : p)
         if (x) (void)hipFree(x);
     acc = TwoLevelAccel{};

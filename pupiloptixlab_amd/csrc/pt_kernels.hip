@@ -617,8 +617,12 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     bsdf.type = MAT;
 
     bool alive = true;
+    bool L_changed = false;  // rad is rewritten only when this hit adds emission
     if (bounce == 0) {
-        if (hg.emitter >= 0) L = L + emitter_radiance(sc.areas[hg.emitter], geo.texcoord);  // main.cu:88-92
+        if (hg.emitter >= 0) {  // main.cu:88-92
+            L = L + emitter_radiance(sc.areas[hg.emitter], geo.texcoord);
+            L_changed = true;
+        }
         const float test = rng_next(rng);                                                    // main.cu:101
         uint32_t l;
         if (last_sample(fp, p, l)) {
@@ -644,6 +648,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         if (!is_zero(pdf_e)) {
             const float mis = (flags >> 31) ? 1.f : mis_weight(prev_pdf, pdf_e * e.select_probability);
             L = L + T * Le * mis;
+            L_changed = true;
         }
     }
 
@@ -708,10 +713,22 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     // the shadow ray starts where the extension ray does (main.cu:119-123,158): one origin
     // record for both, w = the shadow ray's tmax (the extension ray's tmax is a constant)
     if (push_shadow || push_next) ps.ray_o[p] = f4(geo.position, sh_tmax);
+#if PUPIL_SHADE_SKIP
+    // A path that spawns no extension ray is never shaded again: its throughput and misc
+    // records are dead (the shadow retire reads only sh_c and rad, the accumulate only
+    // rad), and rad is rewritten only when this hit added emission.
+    if (push_next) {
+        ps.thr[p] = f4(T, pdf_b);
+        ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
+                                __float_as_uint(geo.texcoord.y));
+    }
+    if (L_changed) ps.rad[p] = f4(L, 0.f);
+#else
     ps.thr[p] = f4(T, pdf_b);
     ps.rad[p] = f4(L, 0.f);
     ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
                             __float_as_uint(geo.texcoord.y));
+#endif
     return (push_next ? 1u : 0u) | (push_shadow ? 2u : 0u) | (nee ? 4u : 0u);
 }
 
@@ -751,7 +768,7 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
     }
 }
 
-// All shading of a bounce in one launch.  The material bins lie back to back in
+// All shading of a bounce in one launch (4 waves per SIMD: <= 128 VGPRs).  The material bins lie back to back in
 // q.bins (bin 0 = miss, 1..7 = EMatType, 8 = unknown type), each in increasing
 // path order, so a wave sees one material except at the 8 bin boundaries; the
 // branch below is wave-uniform almost everywhere.  One launch instead of nine
@@ -764,7 +781,7 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
 // partition launches.  Each path's bounce comes from its own state, so the paths of
 // several frames in flight (pipelined renders, engine.hip) share one launch.
 template <int LIST>
-__global__ __launch_bounds__(kShadeBlock) void k_shade_all(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
+__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_shade_all(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
                                                            uint32_t tag, uint32_t range_base, uint32_t range_n) {
     const uint32_t n_list = LIST == kShadeNext || LIST == kShadeNextRange ? q.counts[kCntNext] : 0u;
     const uint32_t count = LIST == kShadeBins ? q.counts[kScratch]  // all traced paths (total of the bin partition)
