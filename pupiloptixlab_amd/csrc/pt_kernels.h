@@ -90,15 +90,7 @@ struct Queues {
 enum PartMode : int {
     kPartExclusive = 0,  // bin = key >> shift (0xFF = none)
     kPartFlags = 1,      // bin b <=> bit b of the key, if key >> 2 == tag (passed as `shift`)
-    // kPartFlags with both lists band-major: bin b < kBands = extension rays of the paths
-    // in image row band b, bin kBands + b = their shadow rays (band of path i: its local
-    // pixel i % num_local, cut into kBands equal ranges); reported as kPartFlags's two
-    // bins, so each list runs band after band and every XCD's dequeue chunk (1/8 of a
-    // list) covers about one band of the image instead of whole sample images
-    kPartFlagsBand = 2,
 };
-constexpr uint32_t kBands = 8;
-constexpr int kPartMaxBinsAll = 2 * kBands;  // bins of any partition mode (scratch sizing)
 
 struct FrameParams {
     uint32_t width, height;
@@ -186,10 +178,9 @@ void launch_debug_select(const DeviceScene &sc, const float *p, int *out, uint32
 uint32_t partition_hist_entries(uint32_t n);
 // log_out (or null): the nbins counts; cum_out (or null): the counts are added to these
 // nbins running 64-bit totals (rays traced since the engine was created)
-// num_local: kPartFlagsBand's pixels per sample image (path i's local pixel = i % num_local)
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
                       uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, uint32_t *log_out,
-                      hipStream_t s, unsigned long long *cum_out = nullptr, uint32_t num_local = 0);
+                      hipStream_t s, unsigned long long *cum_out = nullptr);
 
 // LBVH builder (bvh_build.hip)
 struct BvhBuildInput {
