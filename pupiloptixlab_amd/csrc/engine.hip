@@ -92,6 +92,10 @@ struct pupil_pt {
     uint32_t bvh_width = 4;  // flattened BVH node format (PUPIL_BVH_WIDTH)
     bool primary_interleave = true;  // primary extend dequeues pixel-major (PUPIL_PRIMARY_ORDER)
     bool shade_list = false;  // shade walks the traced list instead of a material partition (PUPIL_SHADE_LIST)
+    // list shading: a fresh batch's generate stores only its camera rays, and its bounce-0 shade
+    // derives throughput, radiance and RNG (PUPIL_FRESH_SHADE=0: generate stores them all)
+    bool fresh_shade = true;
+    bool fresh() const { return fresh_shade && shade_list; }
     TwoLevelAccel tl{};
     uint32_t width = 0, height = 0, max_depth = 1;
     uint32_t num_prims = 0;
@@ -485,7 +489,7 @@ int render_classic(RenderCtx &cx, const FrameParams &fp) {
                          q.counts + kStartBins, q.counts + kScratch, nullptr, s);
     };
     const uint32_t interleave = pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u;
-    launch_generate(pt->sc, fp, ps, s);
+    launch_generate(pt->sc, fp, ps, s, !pt->fresh());
     cx.ev0(0);
     cx.tail_slot();
     // camera rays: the spp samples of a pixel on consecutive lanes (PUPIL_PRIMARY_ORDER=path: path order)
@@ -498,7 +502,7 @@ int render_classic(RenderCtx &cx, const FrameParams &fp) {
         if (tag == 0) HIP_TRY(hipMemsetAsync(ps.sflags, 0, np, s));
         cx.ev0(2);
         launch_shade(pt->sc, fp, ps, q, tag, s, !pt->shade_list ? kShadeBins : (b == 0 ? kShadeAll : kShadeNext), 0u,
-                     np, np);
+                     np, np, pt->fresh(), fp.seed0);
         cx.ev1();
         if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
             // next (bit 0) and shadow (bit 1) lists -> q.nxsh, each in increasing path order
@@ -618,7 +622,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
             }
             FrameParams fg = fp;
             fg.seed0 = nf.seed;
-            launch_generate(pt->sc, fg, cx.view(nf.slot, np), s);
+            launch_generate(pt->sc, fg, cx.view(nf.slot, np), s, !pt->fresh());
             started++;
         }
         if (had) {
@@ -658,7 +662,8 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         const uint32_t max_count = (uint32_t)std::min<uint64_t>(
             nring, (had ? (uint64_t)pt->pipe.size() * np : 0u) + (inject ? np : 0u));
         cx.ev0(2);
-        launch_shade(pt->sc, fs, ring, q, wtag, s, list, (uint32_t)(nf.slot * np), inject ? (uint32_t)np : 0u, max_count);
+        launch_shade(pt->sc, fs, ring, q, wtag, s, list, (uint32_t)(nf.slot * np), inject ? (uint32_t)np : 0u, max_count,
+                     pt->fresh(), nf.seed);
         cx.ev1();
         pt->pipe_gen++;
         for (auto &f : pt->pipe) f.phases++;
@@ -913,6 +918,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         }
         sc.single_bin = pt->shade_list && bins && (bins & (bins - 1u)) == 0u ? (uint32_t)__builtin_ctz(bins) : 0u;
     }
+    if (const char *fr = std::getenv("PUPIL_FRESH_SHADE")) pt->fresh_shade = std::atoi(fr) != 0;
     pt->mixed_trace = true;
     if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
     if (const char *a = std::getenv("PUPIL_AHEAD")) pt->ahead_mode = std::min(2, std::max(0, std::atoi(a)));

@@ -131,7 +131,8 @@ struct TraceStats {
 };
 
 // wavefront stages
-void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, hipStream_t s);
+// full = false: only the camera rays (the list shade then treats the batch as fresh paths)
+void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, hipStream_t s, bool full);
 // interleave_spp / num_local (primary extend, queue == null): dequeue the spp samples of
 // a pixel on consecutive lanes (TraceJob::spp); 0 = path order
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
@@ -144,9 +145,13 @@ void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, 
 // Each path's bounce is read from its state (PathState::misc.y), so one launch may shade
 // paths of several frames at different bounces; `tag` is the bounce tag the launch writes
 // into the flags bytes (sflag_tag, or the pipeline's generation tag).
+// fresh_range (list modes): the range is a batch whose k_generate stored only its camera rays
+// (full = false), first frame seed fresh_seed0; its bounce-0 shade derives throughput 1,
+// radiance 0 and the camera RNG instead of reading them.
 enum ShadeList : int { kShadeBins = 0, kShadeAll = 1, kShadeNext = 2, kShadeNextRange = 3 };
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q, uint32_t tag,
-                  hipStream_t s, ShadeList list, uint32_t range_base, uint32_t range_n, uint32_t max_count);
+                  hipStream_t s, ShadeList list, uint32_t range_base, uint32_t range_n, uint32_t max_count,
+                  bool fresh_range = false, uint32_t fresh_seed0 = 0);
 void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                    const TraceStats *stats, hipStream_t s);
 // one persistent launch over the next + shadow lists of a bounce (BVH4 persistent path only)

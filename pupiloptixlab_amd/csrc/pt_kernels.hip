@@ -428,17 +428,30 @@ __device__ __forceinline__ uint32_t global_pixel(const FrameParams &fp, uint32_t
     return fp.pixel_map ? fp.pixel_map[l] : l;
 }
 
-__global__ __launch_bounds__(kShadeBlock) void k_generate(DeviceScene sc, FrameParams fp, PathState ps) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= fp.num_paths) return;
+// A fresh path's RNG after the camera ray's two draws (main.cu:53-55): path p of a batch whose
+// first frame has seed seed0 (sample p / num_local, local pixel p % num_local)
+__device__ __forceinline__ uint32_t camera_rng(const FrameParams &fp, uint32_t p, uint32_t seed0, float &jx,
+                                               float &jy, uint32_t &pixel) {
     const uint32_t s = p / fp.num_local;
     const uint32_t l = p - s * fp.num_local;
-    const uint32_t pixel = global_pixel(fp, l);
+    pixel = global_pixel(fp, l);
+    uint32_t rng = rng_init(pixel, seed0 + s);  // main.cu:53
+    jx = rng_next(rng);                         // main.cu:55 (x drawn first)
+    jy = rng_next(rng);
+    return rng;
+}
+
+// full = 0 (list shading, PUPIL_FRESH_SHADE): only the camera ray is stored; the bounce-0
+// shade of the fresh paths takes throughput 1, radiance 0 and the RNG from camera_rng
+// instead of reading them (k_shade_all `fresh`)
+__global__ __launch_bounds__(kShadeBlock) void k_generate(DeviceScene sc, FrameParams fp, PathState ps, uint32_t full) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= fp.num_paths) return;
+    float jx, jy;
+    uint32_t pixel;
+    const uint32_t rng = camera_rng(fp, p, fp.seed0, jx, jy, pixel);
     const uint32_t y = pixel / fp.width;
     const uint32_t x = pixel - y * fp.width;
-    uint32_t rng = rng_init(pixel, fp.seed0 + s);  // main.cu:53
-    const float jx = rng_next(rng);                 // main.cu:55 (x drawn first)
-    const float jy = rng_next(rng);
     const vec4 film = v4(((float)x + jx) / (float)fp.width, ((float)y + jy) / (float)fp.height, 0.f, 1.f);
     const float *m = sc.camera.s2c;
     vec4 d = v4(dot(v4(m[0], m[1], m[2], m[3]), film), dot(v4(m[4], m[5], m[6], m[7]), film),
@@ -452,6 +465,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_generate(DeviceScene sc, FrameP
                                   dot(v4(c[8], c[9], c[10], c[11]), d)));
     ps.ray_o[p] = make_float4(c[3], c[7], c[11], 0.f);
     ps.ray_d[p] = make_float4(dir.x, dir.y, dir.z, 0.f);
+    if (!full) return;
     ps.thr[p] = make_float4(1.f, 1.f, 1.f, 0.f);
     ps.rad[p] = make_float4(0.f, 0.f, 0.f, 0.f);
     ps.misc[p] = make_uint4(rng, 0u, 0u, 0u);
@@ -589,22 +603,24 @@ __device__ __forceinline__ bool last_sample(const FrameParams &fp, uint32_t p, u
     return q % fp.spp + 1u == fp.spp;
 }
 
+// fresh: a path of the frame generated for this launch (bounce 0, throughput 1, radiance 0,
+// RNG `fresh_rng`; k_generate stored only its camera ray)
 template <uint32_t MAT>
 __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
-                                              uint32_t p) {
+                                              uint32_t p, bool fresh, uint32_t fresh_rng) {
     bool push_next = false, push_shadow = false;
     const float4 h = ps.hit[p];
     const float4 o4 = ps.ray_o[p];
     const float4 d4 = ps.ray_d[p];
     const vec3 ray_o = f3(o4), ray_d = f3(d4);
-    const uint4 misc = ps.misc[p];
+    const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ps.misc[p];
     uint32_t rng = misc.x;
     const uint32_t flags = misc.y;
     const uint32_t bounce = flags & 0xFFFFFFu;
-    float4 thr4 = ps.thr[p];
+    float4 thr4 = fresh ? make_float4(1.f, 1.f, 1.f, 0.f) : ps.thr[p];
     vec3 T = f3(thr4);
     const float prev_pdf = thr4.w;
-    float4 rad4 = ps.rad[p];
+    float4 rad4 = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ps.rad[p];
     vec3 L = f3(rad4);
     const vec2 stale_uv = v2(__uint_as_float(misc.z), __uint_as_float(misc.w));
 
@@ -617,7 +633,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     bsdf.type = MAT;
 
     bool alive = true;
-    bool L_changed = false;  // rad is rewritten only when this hit adds emission
+    bool L_changed = fresh;  // rad is rewritten only when this hit adds emission (or was never stored)
     if (bounce == 0) {
         if (hg.emitter >= 0) {  // main.cu:88-92
             L = L + emitter_radiance(sc.areas[hg.emitter], geo.texcoord);
@@ -735,10 +751,10 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
 // Paths whose ray left the scene (__miss__default, main.cu:196-212, and the
 // env handling at main.cu:87-99 / 165-169).
 __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
-                                           uint32_t p) {
-    const uint4 misc = ps.misc[p];
+                                           uint32_t p, bool fresh, uint32_t fresh_rng) {
+    const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ps.misc[p];
     if ((misc.y & 0xFFFFFFu) == 0u) {
-        float4 rad4 = ps.rad[p];
+        float4 rad4 = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ps.rad[p];
         vec3 L = f3(rad4);
         uint32_t rng = misc.x;
         if (sc.has_env) {
@@ -782,7 +798,8 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
 // several frames in flight (pipelined renders, engine.hip) share one launch.
 template <int LIST>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_shade_all(DeviceScene sc, FrameParams fp, PathState ps, Queues q,
-                                                           uint32_t tag, uint32_t range_base, uint32_t range_n) {
+                                                           uint32_t tag, uint32_t range_base, uint32_t range_n,
+                                                           uint32_t fresh_range, uint32_t fresh_seed0) {
     const uint32_t n_list = LIST == kShadeNext || LIST == kShadeNextRange ? q.counts[kCntNext] : 0u;
     const uint32_t count = LIST == kShadeBins ? q.counts[kScratch]  // all traced paths (total of the bin partition)
                                               : n_list + (LIST == kShadeAll || LIST == kShadeNextRange ? range_n : 0u);
@@ -803,17 +820,30 @@ __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))
         } else {
             bin = ps.mbin[p];
         }
+        // the range part of a list launch is a fresh frame; with fresh_range its paths'
+        // throughput, radiance and RNG were never stored (k_generate full = 0)
+        const bool fresh = LIST != kShadeBins && fresh_range && i >= n_list;
+        uint32_t fresh_rng = 0;
+        if (fresh) {
+            float jx, jy;
+            uint32_t pixel;
+            fresh_rng = camera_rng(fp, p - range_base, fresh_seed0, jx, jy, pixel);
+        }
         uint32_t flags = 0;
         switch (bin) {
-        case 0: shade_miss(sc, fp, ps, p); break;
-        case PUPIL_MAT_DIFFUSE: flags = shade_hit<PUPIL_MAT_DIFFUSE>(sc, fp, ps, p); break;
-        case PUPIL_MAT_DIELECTRIC: flags = shade_hit<PUPIL_MAT_DIELECTRIC>(sc, fp, ps, p); break;
-        case PUPIL_MAT_ROUGH_DIELECTRIC: flags = shade_hit<PUPIL_MAT_ROUGH_DIELECTRIC>(sc, fp, ps, p); break;
-        case PUPIL_MAT_CONDUCTOR: flags = shade_hit<PUPIL_MAT_CONDUCTOR>(sc, fp, ps, p); break;
-        case PUPIL_MAT_ROUGH_CONDUCTOR: flags = shade_hit<PUPIL_MAT_ROUGH_CONDUCTOR>(sc, fp, ps, p); break;
-        case PUPIL_MAT_PLASTIC: flags = shade_hit<PUPIL_MAT_PLASTIC>(sc, fp, ps, p); break;
-        case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p); break;
-        default: flags = shade_hit<0u>(sc, fp, ps, p); break;
+        case 0: shade_miss(sc, fp, ps, p, fresh, fresh_rng); break;
+        case PUPIL_MAT_DIFFUSE: flags = shade_hit<PUPIL_MAT_DIFFUSE>(sc, fp, ps, p, fresh, fresh_rng); break;
+        case PUPIL_MAT_DIELECTRIC: flags = shade_hit<PUPIL_MAT_DIELECTRIC>(sc, fp, ps, p, fresh, fresh_rng); break;
+        case PUPIL_MAT_ROUGH_DIELECTRIC:
+            flags = shade_hit<PUPIL_MAT_ROUGH_DIELECTRIC>(sc, fp, ps, p, fresh, fresh_rng);
+            break;
+        case PUPIL_MAT_CONDUCTOR: flags = shade_hit<PUPIL_MAT_CONDUCTOR>(sc, fp, ps, p, fresh, fresh_rng); break;
+        case PUPIL_MAT_ROUGH_CONDUCTOR:
+            flags = shade_hit<PUPIL_MAT_ROUGH_CONDUCTOR>(sc, fp, ps, p, fresh, fresh_rng);
+            break;
+        case PUPIL_MAT_PLASTIC: flags = shade_hit<PUPIL_MAT_PLASTIC>(sc, fp, ps, p, fresh, fresh_rng); break;
+        case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p, fresh, fresh_rng); break;
+        default: flags = shade_hit<0u>(sc, fp, ps, p, fresh, fresh_rng); break;
         }
         if (fp.nee_count) {  // collect_stats only: the reference's shadow-ray count, one atomic per wave
             const unsigned long long m = __ballot((flags & 4u) != 0u);
@@ -943,9 +973,9 @@ void launch_debug_math(const float *x, const float *y2, float *out, uint32_t n, 
 // ------------------------------------------------------------------ launchers
 uint32_t trace_grid_blocks() { return 256u * 16u; }
 
-void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, hipStream_t s) {
+void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, hipStream_t s, bool full) {
     const uint32_t blocks = (fp.num_paths + kShadeBlock - 1) / kShadeBlock;
-    hipLaunchKernelGGL(k_generate, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps);
+    hipLaunchKernelGGL(k_generate, dim3(blocks), dim3(kShadeBlock), 0, s, sc, fp, ps, full ? 1u : 0u);
 }
 
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
@@ -996,9 +1026,12 @@ static uint32_t shade_blocks(uint32_t num_paths) {
 
 // max_count: host bound on the paths the launch may list (the device knows the count)
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q, uint32_t tag,
-                  hipStream_t s, ShadeList list, uint32_t range_base, uint32_t range_n, uint32_t max_count) {
+                  hipStream_t s, ShadeList list, uint32_t range_base, uint32_t range_n, uint32_t max_count,
+                  bool fresh_range, uint32_t fresh_seed0) {
     const dim3 g(shade_blocks(max_count)), b(kShadeBlock);
-#define SHADE(L) hipLaunchKernelGGL(k_shade_all<L>, g, b, 0, s, sc, fp, ps, q, tag, range_base, range_n)
+    const uint32_t fr = fresh_range && list != kShadeBins ? 1u : 0u;
+#define SHADE(L) \
+    hipLaunchKernelGGL(k_shade_all<L>, g, b, 0, s, sc, fp, ps, q, tag, range_base, range_n, fr, fresh_seed0)
     switch (list) {
     case kShadeAll: SHADE(kShadeAll); break;
     case kShadeNext: SHADE(kShadeNext); break;
