@@ -586,27 +586,6 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
         } else if (gpu_tlas) {
             std::vector<uint32_t> order;
             if (build_bvh4_over_boxes(&eb[0].lo[0], (uint32_t)eb.size(), nodes, order, &depth, s) != 0) return -1;
-            // PUPIL_TL_ORDER=dfs (A/B): TLAS nodes renumbered in preorder (still parents first)
-            const char *to = std::getenv("PUPIL_TL_ORDER");
-            if (to && std::strcmp(to, "dfs") == 0 && nodes.size() > 1) {
-                std::vector<uint32_t> nid(nodes.size(), 0xFFFFFFFFu), stack{0u};
-                uint32_t next = 0;
-                while (!stack.empty()) {
-                    const uint32_t v = stack.back();
-                    stack.pop_back();
-                    nid[v] = next++;
-                    for (int k = 3; k >= 0; k--)
-                        if (nodes[v].child[k] >= 0 && nodes[v].child[k] != kEmptyLink) stack.push_back((uint32_t)nodes[v].child[k]);
-                }
-                std::vector<Bvh4Node> o(nodes.size());
-                for (size_t v = 0; v < nodes.size(); v++) {
-                    Bvh4Node nd = nodes[v];
-                    for (int k = 0; k < 4; k++)
-                        if (nd.child[k] >= 0 && nd.child[k] != kEmptyLink) nd.child[k] = (int)nid[nd.child[k]];
-                    o[nid[v]] = nd;
-                }
-                nodes.swap(o);
-            }
             for (Bvh4Node &nd : nodes)
                 for (int k = 0; k < 4; k++)
                     if (nd.child[k] < 0) nd.child[k] = links[order[leaf_first(nd.child[k])]];

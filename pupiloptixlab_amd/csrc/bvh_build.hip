@@ -1234,68 +1234,6 @@ void free_lbvh(BvhBuildOutput &out) {
     out.attrs = nullptr;
 }
 
-// Node order of the BVH4 in memory (PUPIL_NODE_ORDER, A/B).  The collapse emits
-// nodes breadth first (siblings adjacent, a subtree spread over every level
-// below it).  "dfs": preorder; "kids": preorder that places each node's inner
-// children next to each other before descending (siblings adjacent and a
-// subtree contiguous).  Links are remapped; leaves and the root (0) keep theirs.
-hipError_t relabel_nodes4(Bvh4Node *d_nodes, uint32_t n, const char *order, hipStream_t s) {
-    const bool kids = std::strcmp(order, "kids") == 0;
-    if (!kids && std::strcmp(order, "dfs") != 0) return hipSuccess;
-    std::vector<Bvh4Node> h(n), o(n);
-    hipError_t err = hipMemcpyAsync(h.data(), d_nodes, sizeof(Bvh4Node) * n, hipMemcpyDeviceToHost, s);
-    if (!err) err = hipStreamSynchronize(s);
-    if (err) return err;
-    std::vector<int> nid(n, -1);
-    int next = 0;
-    std::vector<int> stack{0};
-    nid[0] = next++;
-    while (!stack.empty()) {
-        const int v = stack.back();
-        stack.pop_back();
-        const Bvh4Node &nd = h[v];
-        if (kids) {
-            for (int k = 0; k < 4; k++) {
-                const int c = nd.child[k];
-                if (c >= 0 && c != kEmptyLink && nid[c] < 0) nid[c] = next++;
-            }
-            for (int k = 3; k >= 0; k--) {
-                const int c = nd.child[k];
-                if (c >= 0 && c != kEmptyLink) stack.push_back(c);
-            }
-        } else {
-            for (int k = 3; k >= 0; k--) {
-                const int c = nd.child[k];
-                if (c >= 0 && c != kEmptyLink && nid[c] < 0) stack.push_back(c);
-            }
-            if (nid[v] < 0) nid[v] = next++;
-        }
-    }
-    if (!kids) {  // preorder: number on pop
-        std::fill(nid.begin(), nid.end(), -1);
-        next = 0;
-        stack.assign(1, 0);
-        while (!stack.empty()) {
-            const int v = stack.back();
-            stack.pop_back();
-            nid[v] = next++;
-            for (int k = 3; k >= 0; k--) {
-                const int c = h[v].child[k];
-                if (c >= 0 && c != kEmptyLink) stack.push_back(c);
-            }
-        }
-    }
-    for (uint32_t v = 0; v < n; v++) {
-        if (nid[v] < 0) return hipErrorUnknown;  // unreachable node: cannot happen
-        Bvh4Node nd = h[v];
-        for (int k = 0; k < 4; k++)
-            if (nd.child[k] >= 0 && nd.child[k] != kEmptyLink) nd.child[k] = nid[nd.child[k]];
-        o[nid[v]] = nd;
-    }
-    err = hipMemcpyAsync(d_nodes, o.data(), sizeof(Bvh4Node) * n, hipMemcpyHostToDevice, s);
-    return err ? err : hipStreamSynchronize(s);
-}
-
 int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s, double *build_ms,
                bool force_lbvh) {
     const int n = (int)in.num_prims;
@@ -1399,11 +1337,6 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
                     err = collapse_bvh4(n, vi, boxes, children, ranges, node_boxes, leaf_size, out.nodes4,
                                         &out.num_nodes4, &out.depth4, &out.level_start, s,
                                         !(collapse && std::strcmp(collapse, "greedy") == 0));
-                const char *order = std::getenv("PUPIL_NODE_ORDER");
-                if (!err && order && out.num_nodes4 > 1) {
-                    err = relabel_nodes4(out.nodes4, out.num_nodes4, order, s);
-                    out.level_start.clear();  // no longer breadth first
-                }
             } else if (!err) {
             // 4-wide quantized tree: depth parity -> flags -> compact indices -> nodes
             uint32_t *depth = ko, *flags4 = vo, *idx4 = nullptr;  // the sort's free ping-pong buffers
