@@ -114,6 +114,49 @@ struct FrameParams {
     uint32_t aov_local;
 };
 
+// Path-state records are streamed with non-temporal loads / stores (PUPIL_NT, A/B builds: 0),
+// so the GBs of path state a step moves do not push BVH nodes and primitive records out of
+// the L2s and the Infinity Cache.
+#ifndef PUPIL_NT
+#define PUPIL_NT 1
+#endif
+__device__ __forceinline__ float4 ld_ps(const float4 *a) {
+#if PUPIL_NT
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(a));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *a;
+#endif
+}
+__device__ __forceinline__ uint4 ld_ps(const uint4 *a) {
+#if PUPIL_NT
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(a));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *a;
+#endif
+}
+__device__ __forceinline__ void st_ps(float4 *a, float4 v) {
+#if PUPIL_NT
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    v4f w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<v4f *>(a));
+#else
+    *a = v;
+#endif
+}
+__device__ __forceinline__ void st_ps(uint4 *a, uint4 v) {
+#if PUPIL_NT
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    v4u w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(a));
+#else
+    *a = v;
+#endif
+}
+
 // shade: a path that spawns no extension ray skips its dead thr / misc stores, and rad is
 // stored only when the hit added emission (A/B builds: -DPUPIL_SHADE_SKIP=0)
 #ifndef PUPIL_SHADE_SKIP

@@ -156,14 +156,14 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     float4 o, d;
                     if (MODE == kModeExtend) {
                         p = job.queue ? job.queue[i] : (job.spp ? (i % job.spp) * job.num_local + i / job.spp : i);
-                        o = ps.ray_o[p];
-                        d = ps.ray_d[p];
+                        o = ld_ps(ps.ray_o + p);
+                        d = ld_ps(ps.ray_d + p);
                         tmin = 0.001f;
                         tmax = kMaxDistance;
                     } else if (MODE == kModeShadow) {
                         p = shadow_q[i];
-                        o = ps.ray_o[p];  // shadow rays share the origin record, w = tmax
-                        d = ps.sh_d[p];
+                        o = ld_ps(ps.ray_o + p);  // shadow rays share the origin record, w = tmax
+                        d = ld_ps(ps.sh_d + p);
                         tmin = 0.001f;
                         tmax = o.w;
                     } else if (MODE == kModeMixedAhead && k < len_a) {
@@ -172,15 +172,15 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         const uint32_t j = lo_a + k;
                         p = (job.spp ? (j % job.spp) * job.num_local + j / job.spp : j) + job.ahead_base;
                         any = false;
-                        o = ps.ray_o[p];
-                        d = ps.ray_d[p];
+                        o = ld_ps(ps.ray_o + p);
+                        d = ld_ps(ps.ray_d + p);
                         tmin = 0.001f;
                         tmax = kMaxDistance;
                     } else if (kMixed) {
                         p = q.nxsh[i] + (MODE == kModeMixedAhead ? job.list_base : 0u);
                         any = i >= n_next;
-                        o = ps.ray_o[p];
-                        d = any ? ps.sh_d[p] : ps.ray_d[p];
+                        o = ld_ps(ps.ray_o + p);
+                        d = any ? ld_ps(ps.sh_d + p) : ld_ps(ps.ray_d + p);
                         tmin = 0.001f;
                         tmax = any ? o.w : kMaxDistance;
                     } else {
@@ -332,7 +332,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 // hit index: the record (flat) or the global primitive id (two-level shading,
                 // reconstruct(); the world-mode flat kernel keeps it in best_key)
                 const uint32_t hidx = !TL && sc.two_level ? best_key : best_idx;
-                ps.hit[p] = make_float4(found ? tmax : -1.f, b1, b2, __uint_as_float(found ? hidx : kMissIndex));
+                st_ps(ps.hit + p, make_float4(found ? tmax : -1.f, b1, b2, __uint_as_float(found ? hidx : kMissIndex)));
                 // single-material scenes: shading reads the bin off the hit (no dependent
                 // record fetch here, which would stall the wave before its next refill)
                 if (found && sc.single_bin == 0u) {
@@ -348,12 +348,12 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         }
         if (MODE == kModeShadow || kMixed) {
             if (done && any && !found) {  // main.cu:124-139
-                const float4 c = ps.sh_c[p];
-                float4 L = ps.rad[p];
+                const float4 c = ld_ps(ps.sh_c + p);
+                float4 L = ld_ps(ps.rad + p);
                 L.x = L.x + c.x;
                 L.y = L.y + c.y;
                 L.z = L.z + c.z;
-                ps.rad[p] = L;
+                st_ps(ps.rad + p, L);
             }
         } else if (MODE == kModeRays && done) {
             float *o = job.out + 4 * (size_t)p;
@@ -463,12 +463,12 @@ __global__ __launch_bounds__(kShadeBlock) void k_generate(DeviceScene sc, FrameP
     const float *c = sc.camera.c2w;
     const vec3 dir = normalize(v3(dot(v4(c[0], c[1], c[2], c[3]), d), dot(v4(c[4], c[5], c[6], c[7]), d),
                                   dot(v4(c[8], c[9], c[10], c[11]), d)));
-    ps.ray_o[p] = make_float4(c[3], c[7], c[11], 0.f);
-    ps.ray_d[p] = make_float4(dir.x, dir.y, dir.z, 0.f);
+    st_ps(ps.ray_o + p, make_float4(c[3], c[7], c[11], 0.f));
+    st_ps(ps.ray_d + p, make_float4(dir.x, dir.y, dir.z, 0.f));
     if (!full) return;
-    ps.thr[p] = make_float4(1.f, 1.f, 1.f, 0.f);
-    ps.rad[p] = make_float4(0.f, 0.f, 0.f, 0.f);
-    ps.misc[p] = make_uint4(rng, 0u, 0u, 0u);
+    st_ps(ps.thr + p, make_float4(1.f, 1.f, 1.f, 0.f));
+    st_ps(ps.rad + p, make_float4(0.f, 0.f, 0.f, 0.f));
+    st_ps(ps.misc + p, make_uint4(rng, 0u, 0u, 0u));
 }
 
 // ------------------------------------------------------------------ shade
@@ -609,18 +609,18 @@ template <uint32_t MAT>
 __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
                                               uint32_t p, bool fresh, uint32_t fresh_rng) {
     bool push_next = false, push_shadow = false;
-    const float4 h = ps.hit[p];
-    const float4 o4 = ps.ray_o[p];
-    const float4 d4 = ps.ray_d[p];
+    const float4 h = ld_ps(ps.hit + p);
+    const float4 o4 = ld_ps(ps.ray_o + p);
+    const float4 d4 = ld_ps(ps.ray_d + p);
     const vec3 ray_o = f3(o4), ray_d = f3(d4);
-    const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ps.misc[p];
+    const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ld_ps(ps.misc + p);
     uint32_t rng = misc.x;
     const uint32_t flags = misc.y;
     const uint32_t bounce = flags & 0xFFFFFFu;
-    float4 thr4 = fresh ? make_float4(1.f, 1.f, 1.f, 0.f) : ps.thr[p];
+    float4 thr4 = fresh ? make_float4(1.f, 1.f, 1.f, 0.f) : ld_ps(ps.thr + p);
     vec3 T = f3(thr4);
     const float prev_pdf = thr4.w;
-    float4 rad4 = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ps.rad[p];
+    float4 rad4 = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ld_ps(ps.rad + p);
     vec3 L = f3(rad4);
     const vec2 stale_uv = v2(__uint_as_float(misc.z), __uint_as_float(misc.w));
 
@@ -701,8 +701,8 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
                     const float pdf_l = es.pdf * sel_prob;
                     const vec3 C = T * es.radiance * er.f * NoL * mis / pdf_l;
                     sh_tmax = es.distance - 0.001f;
-                    ps.sh_d[p] = f4(es.wi, 0.f);
-                    ps.sh_c[p] = f4(C, 0.f);
+                    st_ps(ps.sh_d + p, f4(es.wi, 0.f));
+                    st_ps(ps.sh_c + p, f4(C, 0.f));
                     push_shadow = true;
                 }
             }
@@ -720,7 +720,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         } else {
             T = T * (br.f * fabs_(br.wi.z) / br.pdf);
             const vec3 nd = to_world(br.wi, geo.normal);
-            ps.ray_d[p] = f4(nd, 0.f);
+            st_ps(ps.ray_d + p, f4(nd, 0.f));
             pdf_b = br.pdf;
             delta = (br.sampled_type & kLobeDelta) ? 1u : 0u;
             push_next = true;
@@ -728,22 +728,22 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     }
     // the shadow ray starts where the extension ray does (main.cu:119-123,158): one origin
     // record for both, w = the shadow ray's tmax (the extension ray's tmax is a constant)
-    if (push_shadow || push_next) ps.ray_o[p] = f4(geo.position, sh_tmax);
+    if (push_shadow || push_next) st_ps(ps.ray_o + p, f4(geo.position, sh_tmax));
 #if PUPIL_SHADE_SKIP
     // A path that spawns no extension ray is never shaded again: its throughput and misc
     // records are dead (the shadow retire reads only sh_c and rad, the accumulate only
     // rad), and rad is rewritten only when this hit added emission.
     if (push_next) {
-        ps.thr[p] = f4(T, pdf_b);
-        ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
-                                __float_as_uint(geo.texcoord.y));
+        st_ps(ps.thr + p, f4(T, pdf_b));
+        st_ps(ps.misc + p, make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
+                                __float_as_uint(geo.texcoord.y)));
     }
-    if (L_changed) ps.rad[p] = f4(L, 0.f);
+    if (L_changed) st_ps(ps.rad + p, f4(L, 0.f));
 #else
-    ps.thr[p] = f4(T, pdf_b);
-    ps.rad[p] = f4(L, 0.f);
-    ps.misc[p] = make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
-                            __float_as_uint(geo.texcoord.y));
+    st_ps(ps.thr + p, f4(T, pdf_b));
+    st_ps(ps.rad + p, f4(L, 0.f));
+    st_ps(ps.misc + p, make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
+                            __float_as_uint(geo.texcoord.y)));
 #endif
     return (push_next ? 1u : 0u) | (push_shadow ? 2u : 0u) | (nee ? 4u : 0u);
 }
@@ -752,15 +752,15 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
 // env handling at main.cu:87-99 / 165-169).
 __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
                                            uint32_t p, bool fresh, uint32_t fresh_rng) {
-    const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ps.misc[p];
+    const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ld_ps(ps.misc + p);
     if ((misc.y & 0xFFFFFFu) == 0u) {
-        float4 rad4 = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ps.rad[p];
+        float4 rad4 = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ld_ps(ps.rad + p);
         vec3 L = f3(rad4);
         uint32_t rng = misc.x;
         if (sc.has_env) {
             vec3 Le;
             float pdf;
-            env_eval(*sc.env, f3(ps.ray_o[p]), f3(ps.ray_d[p]), Le, pdf);
+            env_eval(*sc.env, f3(ld_ps(ps.ray_o + p)), f3(ld_ps(ps.ray_d + p)), Le, pdf);
             L = L + Le;  // main.cu:185, no MIS on the camera ray
         }
         const float test = rng_next(rng);
@@ -771,16 +771,16 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
             if (fp.normal) fp.normal[3 * out] = fp.normal[3 * out + 1] = fp.normal[3 * out + 2] = 0.f;
             if (fp.test) fp.test[out] = test;
         }
-        ps.rad[p] = f4(L, 0.f);
+        st_ps(ps.rad + p, f4(L, 0.f));
     } else if (sc.has_env) {
-        const float4 thr4 = ps.thr[p];
+        const float4 thr4 = ld_ps(ps.thr + p);
         vec3 Le;
         float env_pdf;
-        env_eval(*sc.env, f3(ps.ray_o[p]), f3(ps.ray_d[p]), Le, env_pdf);
+        env_eval(*sc.env, f3(ld_ps(ps.ray_o + p)), f3(ld_ps(ps.ray_d + p)), Le, env_pdf);
         const float mis = mis_weight(thr4.w, env_pdf);  // main.cu:166-167
         const vec3 env_rad = Le * (f3(thr4) * mis);
-        float4 rad4 = ps.rad[p];
-        ps.rad[p] = f4(f3(rad4) + env_rad, 0.f);  // main.cu:185
+        float4 rad4 = ld_ps(ps.rad + p);
+        st_ps(ps.rad + p, f4(f3(rad4) + env_rad, 0.f));  // main.cu:185
     }
 }
 
@@ -816,7 +816,7 @@ __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
             for (int b = 1; b < kPartMaxBins; b++) bin = i >= start[b] ? (uint32_t)b : bin;
         } else if (sc.single_bin) {  // the traversal wrote no bin byte (DeviceScene::single_bin)
-            bin = __float_as_uint(ps.hit[p].w) == kMissIndex ? 0u : sc.single_bin;
+            bin = __float_as_uint(ld_ps(ps.hit + p).w) == kMissIndex ? 0u : sc.single_bin;
         } else {
             bin = ps.mbin[p];
         }
