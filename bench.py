@@ -30,7 +30,7 @@ sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -59,7 +59,9 @@ def parse():
                          "each synchronised) on the same scene exported as XML + OBJ (rank 0, N=1, configs 3/4)")
     ap.add_argument("--save", default="", help="write the frame as PNG (rank 0)")
     ap.add_argument("--dump", default="", help="write the full float32 frame as .npy (rank 0, after the timed steps)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: every rank joins a gloo group, rank 0 prints the ranks seen")
+    args = ap.parse_args(argv)
     defaults = {3: (125, 1920, 1080, 8, 4, 1), 4: (500, 1920, 1080, 8, 4, 1), 5: (125, 3840, 2160, 16, 6, 16)}
     sph, w, h, spp, depth, stride = defaults[args.config]
     args.spheres = sph if args.spheres is None else args.spheres
@@ -70,14 +72,83 @@ def parse():
     args.cpu_sample_stride = stride if args.cpu_sample_stride is None else args.cpu_sample_stride
     return args
 
-def main():
-    args = parse()
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv=None):
+    """`python bench.py --gpus N` without a launcher: start N fresh rank processes of this
+    script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torchrun sets them)
+    and return the exit status.  Runs before anything touches the GPU: this process only
+    spawns and waits (children are started as new processes, never by an exec of this
+    one).  Rank 0 prints the JSON line; a failing rank stops the others."""
+    import subprocess
+
+    argv = list(sys.argv[1:] if argv is None else argv)
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env["MASTER_PORT"] = str(env.get("PUPIL_BENCH_PORT") or free_port())
+    env["WORLD_SIZE"] = env["LOCAL_WORLD_SIZE"] = str(args.gpus)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(args.gpus):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=e))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # one rank failed: the group can never complete
+                    q.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the rank wiring alone (gloo, no GPU): rank 0 prints the ranks that joined."""
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if os.environ.get("PUPIL_BENCH_DRY_FAIL_RANK") == str(rank):  # launcher test: this rank dies
+        sys.exit(3)
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.zeros(max(1, world), dtype=torch.int64)
+    t[rank] = os.getpid()
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_requested": args.gpus,
+                          "ranks_seen": int((t != 0).sum()), "pids": [int(x) for x in t]}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch with --nproc-per-node equal to --gpus)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    import torch
+    import torch.distributed as dist
+
     # rehearsal of the N-rank path on a box with fewer GPUs: PUPIL_BENCH_DEVICES=k maps
     # local rank r to GPU r % k (never set by the driver's runs: one rank per GPU)
     if os.environ.get("PUPIL_BENCH_DEVICES"):
@@ -237,6 +308,7 @@ def main():
         update = {"host_ms": round((time.perf_counter() - t0) * 1e3, 3), "engine_ms": round(pt.stats()["build_ms"], 3)}
 
     if rank == 0:
+        assert world == args.gpus, (world, args.gpus)
         if args.dump:
             np.save(args.dump, last_frame.cpu().numpy())
         if args.save:

@@ -309,7 +309,7 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
 /* copies the flattened BVH4 the traversal kernels read (64-B quantized nodes, 12-float
  * world-space primitive records, root link) to host memory, for the CPU baseline that
  * traverses the same arrays.  Call with nodes = records = NULL for the
- * counts.  PUPIL_ERR_UNSUPPORTED for the two-level structure and the BVH2 / BVH8 formats. */
+ * counts.  PUPIL_ERR_UNSUPPORTED for the two-level structure. */
 int pupil_pt_export_bvh4(pupil_pt *pt, uint32_t *num_nodes, void *nodes, uint32_t *num_records, float *records,
                          int32_t *root_link);
 /* evaluates the device's sin, cos, acos, atan2(x, y2), sqrt, 1/x on n inputs:

@@ -10,8 +10,8 @@
 //                      multisplit ranking (k_sort_hist / k_sort_scan / k_sort_scatter)
 //   5. k_karras        Karras 2012 hierarchy over the sorted codes (index-augmented)
 //   6. k_refit         bottom-up AABBs, agent-scope release/acquire per arrival
-//   7. k_emit          64 B BVH2 nodes; subtrees of <= leaf_size primitives
-//                      collapse into one leaf (their primitives are contiguous)
+//   7. collapse        4-wide quantized nodes (SAH-optimal slot distribution);
+//                      subtrees of <= leaf_size primitives become one leaf
 //   8. k_reorder       primitive records in Morton order (leaf ranges index them)
 //   9. k_attrs         per-primitive shading records in the same order
 #include <hip/hip_runtime.h>
@@ -316,21 +316,6 @@ __device__ __forceinline__ int child_link(int c, const int2 *ranges, uint32_t le
     const uint32_t cnt = (uint32_t)(r.y - r.x + 1);
     if (cnt <= leaf_size) return make_leaf((uint32_t)r.x, cnt);
     return c;
-}
-
-__global__ void k_emit(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
-                       const int2 *ranges, const Aabb *node_boxes, uint32_t leaf_size, BvhNode *nodes) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n - 1) return;
-    const int2 c = children[i];
-    const Aabb a = c.x >= 0 ? node_boxes[c.x] : prim_boxes[sorted_vals[~c.x]];
-    const Aabb b = c.y >= 0 ? node_boxes[c.y] : prim_boxes[sorted_vals[~c.y]];
-    BvhNode nd;
-    nd.lo0 = make_float4(a.lo[0], a.lo[1], a.lo[2], __int_as_float(child_link(c.x, ranges, leaf_size)));
-    nd.hi0 = make_float4(a.hi[0], a.hi[1], a.hi[2], __int_as_float(child_link(c.y, ranges, leaf_size)));
-    nd.lo1 = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f);
-    nd.hi1 = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
-    nodes[i] = nd;
 }
 
 // ---------------------------------------------------------------- PLOC
@@ -833,131 +818,6 @@ __global__ void k_collapse_pick_sah(int items, const int *item_node, const int2 
     inner_count[t] = inner;
 }
 
-// ---------------------------------------------------------------- greedy BVH8 collapse
-// Same greedy surface-area opening as the BVH4 collapse, up to eight children.
-// Each child then gets the slot whose octant best matches its centroid offset
-// from the node centre (slot bit a set <=> offset > 0 on axis a; greedy best
-// score first), so a ray with direction-sign octant o meets the children in
-// roughly front-to-back order by visiting slots in increasing k ^ o.
-constexpr uint32_t kNoPrim = 0xFFFFFFFFu;
-
-__global__ void k_collapse_pick8(int items, const int *item_node, const int2 *children, const int2 *ranges,
-                                 const Aabb *node_boxes, uint32_t leaf_size, int *clist,
-                                 unsigned long long *inner_count) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= items) return;
-    const int b = item_node[t];
-    int c[8];
-    const int2 ch = children[b];
-    c[0] = ch.x;
-    c[1] = ch.y;
-    int nk = 2;
-    while (nk < 8) {
-        int best = -1;
-        float best_a = -1.f;
-        for (int k = 0; k < nk; k++)
-            if (opens(c[k], ranges, leaf_size)) {
-                const float a = half_area(node_boxes[c[k]]);
-                if (a > best_a) {
-                    best_a = a;
-                    best = k;
-                }
-            }
-        if (best < 0) break;
-        const int2 g = children[c[best]];
-        c[best] = g.x;
-        c[nk++] = g.y;
-    }
-    unsigned long long inner = 0;
-    for (int k = 0; k < nk; k++) inner += opens(c[k], ranges, leaf_size) ? 1ull : 0ull;
-    for (int k = 0; k < 8; k++) clist[8 * t + k] = k < nk ? c[k] : kEmptyLink;
-    inner_count[t] = inner;
-}
-
-__global__ void k_collapse_emit8(int items, int base, int next_base, const int *item_node, const int *clist,
-                                 const unsigned long long *inner_pos, const uint32_t *sorted_vals,
-                                 const Aabb *prim_boxes, const int2 *ranges, const Aabb *node_boxes,
-                                 uint32_t leaf_size, int *next_items, Bvh8Node *nodes8, uint32_t *vals8) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= items) return;
-    const Aabb nb = node_boxes[item_node[t]];
-    int cc[8];
-    Aabb cb[8];
-    int nk = 0;
-    for (int k = 0; k < 8; k++) {
-        const int c = clist[8 * t + k];
-        if (c == kEmptyLink) break;
-        cc[nk] = c;
-        cb[nk] = c < 0 ? prim_boxes[sorted_vals[~c]] : node_boxes[c];
-        nk++;
-    }
-    // octant slot assignment, greedy on the score sum_a sign_a(slot) * (centre_a(child) - centre_a(node))
-    int slot_child[8];
-    for (int k = 0; k < 8; k++) slot_child[k] = -1;
-    uint32_t used = 0;
-    for (int round = 0; round < nk; round++) {
-        float best = -__builtin_huge_valf();
-        int bc = -1, bs = -1;
-        for (int i = 0; i < nk; i++) {
-            if ((used >> i) & 1u) continue;
-            float off[3];
-            for (int a = 0; a < 3; a++) off[a] = (cb[i].lo[a] + cb[i].hi[a]) - (nb.lo[a] + nb.hi[a]);
-            for (int sl = 0; sl < 8; sl++) {
-                if (slot_child[sl] >= 0) continue;
-                const float sc = ((sl & 1) ? off[0] : -off[0]) + ((sl & 2) ? off[1] : -off[1]) + ((sl & 4) ? off[2] : -off[2]);
-                if (sc > best || bc < 0) {
-                    best = sc;
-                    bc = i;
-                    bs = sl;
-                }
-            }
-        }
-        slot_child[bs] = bc;
-        used |= 1u << bc;
-    }
-    const uint32_t node = (uint32_t)(base + t);
-    int pos = (int)inner_pos[t];
-    uint32_t imask = 0, pvalid = 0;
-    float clo[3][8], chi[3][8];
-    int nslots = 0;  // slots up to the last used one (quantize_axis_n: k >= nk -> empty)
-    for (int sl = 0; sl < 8; sl++) {
-        const int i = slot_child[sl];
-        if (i < 0) {  // a point at the node's min corner (no imask / pvalid bit: never entered)
-            for (int a = 0; a < 3; a++) clo[a][sl] = chi[a][sl] = nb.lo[a];
-            continue;
-        }
-        nslots = sl + 1;
-        for (int a = 0; a < 3; a++) {
-            clo[a][sl] = cb[i].lo[a];
-            chi[a][sl] = cb[i].hi[a];
-        }
-        const int c = cc[i];
-        if (c >= 0 && opens(c, ranges, leaf_size)) {
-            next_items[pos++] = c;
-            imask |= 1u << sl;
-        } else {
-            const uint32_t first = c < 0 ? (uint32_t)~c : (uint32_t)ranges[c].x;
-            const uint32_t count = c < 0 ? 1u : (uint32_t)(ranges[c].y - ranges[c].x + 1);
-            for (uint32_t j = 0; j < count; j++) {
-                vals8[(size_t)kLeafSlots * node + 2 * sl + j] = sorted_vals[first + j];
-                pvalid |= 1u << (2 * sl + j);
-            }
-        }
-    }
-    Bvh8Node o;
-    uint32_t ex, ey, ez;
-    // slots from nslots on are quantized as empty boxes (lo > hi)
-    quantize_axis_n<8>(nb.lo[0], nb.hi[0], clo[0], chi[0], nslots, o.ox, ex, o.qlo_x, o.qhi_x);
-    quantize_axis_n<8>(nb.lo[1], nb.hi[1], clo[1], chi[1], nslots, o.oy, ey, o.qlo_y, o.qhi_y);
-    quantize_axis_n<8>(nb.lo[2], nb.hi[2], clo[2], chi[2], nslots, o.oz, ez, o.qlo_z, o.qhi_z);
-    o.exps = ex | (ey << 8) | (ez << 16) | (imask << 24);
-    o.child_base = (uint32_t)(next_base + (int)inner_pos[t]);
-    o.pvalid = pvalid;
-    o.pad0[0] = o.pad0[1] = 0u;
-    for (int k = 0; k < 12; k++) o.pad1[k] = 0u;
-    nodes8[node] = o;
-}
-
 // Shading record of each primitive in traversal (Morton) order, kAttrStride
 // float4 per primitive: everything the hit reconstruction of
 // Geometry::GetHitLocalGeometry (render/geometry.h:48-96) gathers from the
@@ -968,10 +828,6 @@ __global__ void k_attrs(int n, const uint32_t *sorted_vals, BvhBuildInput in, fl
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t prim = sorted_vals[i];
-    if (prim == kNoPrim) {  // BVH8 record slot without a primitive
-        for (uint32_t k = 0; k < kAttrStride; k++) attrs[(size_t)kAttrStride * i + k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        return;
-    }
     const uint32_t inst_id = in.prim_inst[prim];
     const DevInstance &inst = in.instances[inst_id];
     // object_space (BLAS): records in the mesh's own primitive order, found by primitive id
@@ -1012,10 +868,6 @@ __global__ void k_reorder(int n, const uint32_t *sorted_vals, const float4 *recs
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t src = sorted_vals[i];
-    if (src == kNoPrim) {  // BVH8 record slot without a primitive (never tested: pvalid bit clear)
-        recs_out[3 * i + 0] = recs_out[3 * i + 1] = recs_out[3 * i + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
-        return;
-    }
     recs_out[3 * i + 0] = recs_in[3 * src + 0];
     recs_out[3 * i + 1] = recs_in[3 * src + 1];
     recs_out[3 * i + 2] = recs_in[3 * src + 2];
@@ -1103,51 +955,6 @@ hipError_t collapse_bvh4(int n, const uint32_t *sorted_vals, const Aabb *prim_bo
     return err;
 }
 
-// Greedy breadth-first BVH8 collapse (k_collapse_pick8 / k_collapse_emit8); nodes8
-// and vals8 (kLeafSlots per node, kNoPrim holes) must hold n - 1 nodes' worth.
-hipError_t collapse_bvh8(int n, const uint32_t *sorted_vals, const Aabb *prim_boxes, const int2 *children,
-                         const int2 *ranges, const Aabb *node_boxes, uint32_t leaf_size, Bvh8Node *nodes8,
-                         uint32_t *vals8, uint32_t *num_nodes8, uint32_t *depth8, hipStream_t s) {
-    int *items_a = nullptr, *items_b = nullptr, *clist = nullptr;
-    unsigned long long *cnt = nullptr, *sums = nullptr, *total = nullptr;
-    const int per = kScanBlock * kScanItems;
-    const int cap = n;
-    hipError_t err = dmalloc(&items_a, cap);
-    if (!err) err = dmalloc(&items_b, cap);
-    if (!err) err = dmalloc(&clist, 8 * (size_t)cap);
-    if (!err) err = dmalloc(&cnt, cap);
-    if (!err) err = dmalloc(&sums, (cap + per - 1) / per);
-    if (!err) err = dmalloc(&total, 1);
-    int base = 0, items = 1;
-    uint32_t levels = 0;
-    if (!err) err = hipMemsetAsync(items_a, 0, sizeof(int), s);  // binary root 0
-    const auto grid = [](int m) { return dim3((unsigned)((m + kBlock - 1) / kBlock)); };
-    while (!err && items > 0) {
-        hipLaunchKernelGGL(k_collapse_pick8, grid(items), dim3(kBlock), 0, s, items, items_a, children, ranges,
-                           node_boxes, leaf_size, clist, cnt);
-        const int nb = (items + per - 1) / per;
-        hipLaunchKernelGGL(k_scan64_blocks, dim3(nb), dim3(kScanBlock), 0, s, cnt, items, sums);
-        hipLaunchKernelGGL(k_scan64_sums, dim3(1), dim3(kScanBlock), 0, s, sums, nb, total);
-        hipLaunchKernelGGL(k_scan64_add, grid(items), dim3(kBlock), 0, s, cnt, items, sums);
-        hipLaunchKernelGGL(k_collapse_emit8, grid(items), dim3(kBlock), 0, s, items, base, base + items, items_a, clist,
-                           cnt, sorted_vals, prim_boxes, ranges, node_boxes, leaf_size, items_b, nodes8, vals8);
-        unsigned long long tot = 0;
-        (void)hipMemcpyAsync(&tot, total, sizeof(tot), hipMemcpyDeviceToHost, s);
-        err = hipStreamSynchronize(s);
-        base += items;
-        items = (int)tot;
-        levels++;
-        if (base + items > n - 1) err = hipErrorUnknown;  // cannot happen
-        std::swap(items_a, items_b);
-    }
-    *num_nodes8 = (uint32_t)base;
-    *depth8 = levels;
-    void *bufs[] = {items_a, items_b, clist, cnt, sums, total};
-    for (void *b : bufs)
-        if (b) (void)hipFree(b);
-    return err;
-}
-
 // PLOC topology (see the PLOC section) -> LBVH arrays and the new primitive order
 hipError_t build_ploc(int n, const uint32_t *vals_in, uint32_t *vals_out, const Aabb *prim_boxes, int2 *children,
                       int2 *ranges, Aabb *node_boxes, int *parent_internal, int *parent_leaf, hipStream_t s) {
@@ -1222,14 +1029,10 @@ hipError_t build_ploc(int n, const uint32_t *vals_in, uint32_t *vals_out, const 
 }  // namespace
 
 void free_lbvh(BvhBuildOutput &out) {
-    if (out.nodes) (void)hipFree(out.nodes);
     if (out.nodes4) (void)hipFree(out.nodes4);
-    if (out.nodes8) (void)hipFree(out.nodes8);
     if (out.prims) (void)hipFree(out.prims);
     if (out.attrs) (void)hipFree(out.attrs);
-    out.nodes = nullptr;
     out.nodes4 = nullptr;
-    out.nodes8 = nullptr;
     out.prims = nullptr;
     out.attrs = nullptr;
 }
@@ -1239,16 +1042,13 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     const int n = (int)in.num_prims;
     if (n <= 0) {  // empty scene: every ray misses
         out = BvhBuildOutput{};
-        out.root_link = out.root_link4 = out.root_link8 = (uint32_t)kTraverseDone;
+        out.root_link4 = (uint32_t)kTraverseDone;
         if (build_ms) *build_ms = 0.0;
         return 0;
     }
     if (leaf_size < 1) leaf_size = 1;
     if (leaf_size > (uint32_t)kLeafMax) leaf_size = kLeafMax;
-    if (in.wide8 && leaf_size > 2) leaf_size = 2;  // two record slots per BVH8 child
     out.depth4 = 0;
-    out.depth8 = 0;
-    out.num_nodes8 = 0;
     out.level_start.clear();
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
@@ -1261,7 +1061,6 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
              *flags = nullptr;
     int2 *children = nullptr, *ranges = nullptr;
     int *parent_internal = nullptr, *parent_leaf = nullptr;
-    uint32_t *vals8 = nullptr;
     const uint32_t nblocks = (uint32_t)((n + kSortTile - 1) / kSortTile);
     hipError_t err = hipSuccess;
     err = dmalloc(&recs, 3 * (size_t)n);
@@ -1278,7 +1077,6 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     if (!err) err = dmalloc(&ranges, n);
     if (!err) err = dmalloc(&parent_internal, n);
     if (!err) err = dmalloc(&parent_leaf, n);
-    if (!err) err = dmalloc(&out.nodes, n > 1 ? (size_t)(n - 1) : 1);
     if (!err) err = dmalloc(&out.prims, 3 * (size_t)n);
     if (!err) err = dmalloc(&out.attrs, (size_t)kAttrStride * n);
     if (err) {
@@ -1317,19 +1115,8 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
                 hipLaunchKernelGGL(k_refit, dim3(g), dim3(kBlock), 0, s, n, vi, boxes, children, parent_internal,
                                    parent_leaf, node_boxes, flags);
             }
-            hipLaunchKernelGGL(k_emit, dim3(gi), dim3(kBlock), 0, s, n, vi, boxes, children, ranges, node_boxes,
-                               leaf_size, out.nodes);
             const char *collapse = std::getenv("PUPIL_BVH4_COLLAPSE");
-            if (!err && in.wide8) {
-                // 8-wide tree; its record order (kLeafSlots slots per node) replaces vi
-                err = dmalloc(&out.nodes8, (size_t)(n - 1));
-                if (!err) err = dmalloc(&vals8, (size_t)kLeafSlots * (n - 1));
-                if (!err) err = hipMemsetAsync(vals8, 0xFF, sizeof(uint32_t) * kLeafSlots * (size_t)(n - 1), s);
-                if (!err)
-                    err = collapse_bvh8(n, vi, boxes, children, ranges, node_boxes, leaf_size, out.nodes8, vals8,
-                                        &out.num_nodes8, &out.depth8, s);
-                out.num_nodes4 = 0;
-            } else if (!err && !(collapse && std::strcmp(collapse, "parity") == 0)) {
+            if (!err && !(collapse && std::strcmp(collapse, "parity") == 0)) {
                 // 4-wide quantized tree: SAH-optimal slot distribution (PUPIL_BVH4_COLLAPSE=greedy:
                 // greedy surface-area opening)
                 err = dmalloc(&out.nodes4, (size_t)(n - 1));
@@ -1365,28 +1152,15 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
         }
         const bool leaf_root = (uint32_t)n <= leaf_size;
         const uint32_t *rec_vals = vi;
-        uint32_t nrec = (uint32_t)n;
-        if (!err && in.wide8 && !leaf_root && out.num_nodes8) {
-            rec_vals = vals8;
-            nrec = kLeafSlots * out.num_nodes8;
-            (void)hipFree(out.prims);
-            (void)hipFree(out.attrs);
-            out.prims = nullptr;
-            out.attrs = nullptr;
-            err = dmalloc(&out.prims, 3 * (size_t)nrec);
-            if (!err) err = dmalloc(&out.attrs, (size_t)kAttrStride * nrec);
-        }
+        const uint32_t nrec = (uint32_t)n;
         if (!err) {
             const uint32_t gr = (nrec + kBlock - 1) / kBlock;
             hipLaunchKernelGGL(k_reorder, dim3(gr), dim3(kBlock), 0, s, (int)nrec, rec_vals, recs, out.prims);
             hipLaunchKernelGGL(k_attrs, dim3(gr), dim3(kBlock), 0, s, (int)nrec, rec_vals, in, out.attrs);
         }
         out.num_records = nrec;
-        out.num_nodes = n > 1 ? (uint32_t)(n - 1) : 0u;
-        if (n == 1 || leaf_root) out.depth4 = out.depth8 = 1;  // the root is a leaf
-        out.root_link = leaf_root ? (uint32_t)make_leaf(0u, (uint32_t)n) : 0u;
-        out.root_link4 = out.root_link;
-        out.root_link8 = out.root_link;
+        if (n == 1 || leaf_root) out.depth4 = 1;  // the root is a leaf
+        out.root_link4 = leaf_root ? (uint32_t)make_leaf(0u, (uint32_t)n) : 0u;
         if (!err) err = hipGetLastError();
     }
     (void)hipEventRecord(e1, s);
@@ -1410,7 +1184,6 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     (void)hipFree(ranges);
     (void)hipFree(parent_internal);
     (void)hipFree(parent_leaf);
-    if (vals8) (void)hipFree(vals8);
     return err == hipSuccess ? 0 : -2;
 }
 
@@ -1486,7 +1259,6 @@ int build_bvh4_over_boxes(const float *h_boxes, uint32_t n, std::vector<Bvh4Node
 int build_bvh_bounded(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s,
                       double *build_ms, uint32_t reserve) {
     const auto fits = [&](const BvhBuildOutput &o) {
-        if (in.wide8) return 2u * o.depth8 + reserve <= (uint32_t)kTrace8StackEntries;  // node + leaf group per level
         return o.depth4 == 0 || 3u * o.depth4 + reserve <= (uint32_t)kTraceStackEntries;
     };
     int rc = build_lbvh(in, out, leaf_size, s, build_ms);

@@ -89,7 +89,6 @@ struct pupil_pt {
     std::vector<void *> allocs;
     BvhBuildOutput bvh{};
     bool two_level = false;  // TLAS + per-shape BLAS (accel_two_level.hip) instead of one flattened BVH
-    uint32_t bvh_width = 4;  // flattened BVH node format (PUPIL_BVH_WIDTH)
     bool primary_interleave = true;  // primary extend dequeues pixel-major (PUPIL_PRIMARY_ORDER)
     bool shade_list = false;  // shade walks the traced list instead of a material partition (PUPIL_SHADE_LIST)
     // list shading: a fresh batch's generate stores only its camera rays, and its bounce-0 shade
@@ -100,7 +99,6 @@ struct pupil_pt {
     uint32_t width = 0, height = 0, max_depth = 1;
     uint32_t num_prims = 0;
     uint32_t leaf_size = 2;  // primitives per BVH leaf (PUPIL_LEAF_SIZE)
-    bool mixed_trace = true;  // one persistent launch per bounce for shadow + extension rays (PUPIL_MIXED)
     // Pipelined frames (render_pipelined, PUPIL_PIPE): the path state is a ring of K
     // slots of one batch each; consecutive renders that continue each other (OnRun
     // cadence, or PUPIL_HINT_CONTINUE) keep up to K frames in flight, each at its own
@@ -397,7 +395,7 @@ uint64_t nodes4_count(const pupil_pt *pt) {
 int refresh_node_bound(pupil_pt *pt) {
     pt->sc.node_bound[0] = pt->sc.node_bound[1] = pt->sc.node_bound[2] = 0.f;
     const uint64_t n = nodes4_count(pt);
-    if (pt->sc.bvh_width != 4 || !pt->sc.nodes4 || n == 0) return PUPIL_OK;
+    if (!pt->sc.nodes4 || n == 0) return PUPIL_OK;
     launch_node_bound(pt->sc.nodes4, n, pt->node_bound, pt->own_stream);
     uint32_t b[3];
     HIP_TRY(hipMemcpyAsync(b, pt->node_bound, sizeof(b), hipMemcpyDeviceToHost, pt->own_stream));
@@ -471,68 +469,6 @@ struct RenderCtx {
     }
 };
 
-// One batch rendered on its own: generate, primary extend, then per bounce shade,
-// flags partition and shadow + extension traversal, then accumulate.  Used by the
-// A/B traversal variants (BVH2 / BVH8 node formats, one ray per lane, PUPIL_MIXED=0).
-int render_classic(RenderCtx &cx, const FrameParams &fp) {
-    pupil_pt *pt = cx.pt;
-    hipStream_t s = cx.s;
-    pt->pipe.clear();
-    pt->pipe_valid = false;
-    int rc = ensure_state(pt, fp.num_paths);
-    if (rc) return rc;
-    const PathState ps = cx.view(0, fp.num_paths);
-    const uint32_t np = fp.num_paths;
-    Queues &q = pt->q;
-    auto bin_paths = [&]() {  // material bins of the traced paths -> q.bins (stable, increasing path id)
-        launch_partition(ps.mbin, np, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
-                         q.counts + kStartBins, q.counts + kScratch, nullptr, s);
-    };
-    const uint32_t interleave = pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u;
-    launch_generate(pt->sc, fp, ps, s, !pt->fresh());
-    cx.ev0(0);
-    cx.tail_slot();
-    // camera rays: the spp samples of a pixel on consecutive lanes (PUPIL_PRIMARY_ORDER=path: path order)
-    launch_extend(pt->sc, ps, q, nullptr, nullptr, np, pt->ovf, pt->ovf_threads, cx.tsp(), s, interleave, fp.num_local);
-    cx.ev1();
-    if (!pt->shade_list) bin_paths();
-    const uint32_t bounces = fp.max_depth;
-    for (uint32_t b = 0; b < bounces; b++) {
-        const uint32_t tag = sflag_tag(fp.max_depth, b);
-        if (tag == 0) HIP_TRY(hipMemsetAsync(ps.sflags, 0, np, s));
-        cx.ev0(2);
-        launch_shade(pt->sc, fp, ps, q, tag, s, !pt->shade_list ? kShadeBins : (b == 0 ? kShadeAll : kShadeNext), 0u,
-                     np, np, pt->fresh(), fp.seed0);
-        cx.ev1();
-        if (b + 1 < bounces) {  // the last shade never spawns shadow or extension rays
-            // next (bit 0) and shadow (bit 1) lists -> q.nxsh, each in increasing path order
-            launch_partition(ps.sflags, np, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
-                             q.counts + kStartNext, nullptr, pt->ray_log + 2 * (b + 1), s, pt->ray_cum);
-            if (pt->mixed_trace && pt->sc.bvh_width >= 4 && pt->sc.trace_refill) {
-                cx.ev0(1);
-                cx.tail_slot();
-                launch_trace_mixed(pt->sc, ps, q, pt->ovf, pt->ovf_threads, cx.tsp(), s);
-                cx.ev1();
-            } else {
-                cx.ev0(1);
-                cx.tail_slot();
-                launch_shadow(pt->sc, ps, q, pt->ovf, pt->ovf_threads, cx.tsp(), s);
-                cx.ev1();
-                cx.ev0(0);
-                cx.tail_slot();
-                launch_extend(pt->sc, ps, q, q.nxsh, q.counts + kCntNext, 0u, pt->ovf, pt->ovf_threads, cx.tsp(), s);
-                cx.ev1();
-            }
-            if (!pt->shade_list) bin_paths();
-        }
-    }
-    launch_accumulate(fp, ps, nullptr, false, s);
-    pt->last_iters = bounces;
-    pt->last_primary = np;
-    pt->primary_cum += np;
-    return PUPIL_OK;
-}
-
 // Pipelined frames.  The batch's path state is one slot of a ring of K slots.  A frame
 // runs max_depth phases -- phase b: trace (b = 0: the camera rays, else the shadow +
 // extension rays its bounce-(b-1) shade spawned) then the bounce-b shade -- and one
@@ -548,8 +484,10 @@ int render_classic(RenderCtx &cx, const FrameParams &fp) {
 // run + 1 iterations of a render (run = renders in a row that continued the previous
 // one), so a continued sequence reaches one iteration per render after K renders, and
 // a render that is never continued (a moving camera) pays only for one frame's first
-// phase ahead.  Per path, every operation and its order are those of render_classic:
-// output is bit-identical.
+// phase ahead.  Per path, every operation and its order are those of the reference's
+// per-pixel loop (main.cu:84-193): output is bit-identical to the oracle whatever the
+// schedule.  Renders that collect counters, depths above 63 (the 6-bit flags tags) and
+// PUPIL_AHEAD=0 run with K = 1: one frame at a time, D iterations.
 int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch *launch) {
     pupil_pt *pt = cx.pt;
     hipStream_t s = cx.s;
@@ -866,9 +804,6 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
             pt->build_ms = pt->tl.build_ms;
         } else {
             BvhBuildInput bin{pt->num_prims, d_prim_inst, d_insts, d_mats};
-            if (const char *w = std::getenv("PUPIL_BVH_WIDTH"))  // node format: 4 (default), 8, or 2 (A/B)
-                pt->bvh_width = (uint32_t)std::atoi(w) == 8 ? 8u : ((uint32_t)std::atoi(w) == 2 ? 2u : 4u);
-            bin.wide8 = pt->bvh_width == 8 ? 1u : 0u;
             const int brc = build_bvh_bounded(bin, pt->bvh, pt->leaf_size, pt->own_stream, &pt->build_ms, 0);
             if (brc == -3) return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "BVH deeper than the traversal stacks hold"));
             if (brc != 0) return cleanup(fail(PUPIL_ERR_HIP, "LBVH build failed"));
@@ -877,11 +812,8 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     pt->h_insts = insts;
     DeviceScene &sc = pt->sc;
     sc.num_prims = pt->num_prims;
-    sc.bvh_width = 4;
     if (pt->two_level) {
         sc.two_level = 1;
-        sc.nodes = nullptr;
-        sc.root_link = (uint32_t)kTraverseDone;
         sc.tl_world = pt->tl.world ? 1u : 0u;
         sc.nodes4 = pt->tl.world ? pt->tl.wnodes : pt->tl.nodes4;
         sc.prims = pt->tl.world ? pt->tl.wprims : pt->tl.prims;
@@ -889,24 +821,18 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         sc.attrs = pt->tl.attrs;
         sc.root_link4 = pt->tl.root_link4;
     } else {
-        sc.nodes = pt->bvh.nodes;
         sc.prims = pt->bvh.prims;
         sc.attrs = pt->bvh.attrs;
-        sc.root_link = pt->bvh.root_link;
         sc.nodes4 = pt->bvh.nodes4;
         sc.root_link4 = pt->bvh.root_link4;
-        sc.nodes8 = pt->bvh.nodes8;
-        sc.root_link8 = pt->bvh.root_link8;
-        sc.bvh_width = pt->bvh_width;
     }
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pt->device);
     sc.num_cus = (uint32_t)std::max(1, cus);
     // persistent BVH4 kernels: refill once 16 lanes are idle (r02 re-tune on the SAH tree:
-    // 16 / 12 beat 20 / 24 by ~0.7 % at N = 1 and the 8-way shard; 0 = one-ray-per-lane A/B)
+    // 16 / 12 beat 20 / 24 by ~0.7 % at N = 1 and the 8-way shard)
     sc.trace_refill = 16;
-    if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(0, std::atoi(r)));
-    if ((pt->two_level || sc.bvh_width == 8) && sc.trace_refill == 0) sc.trace_refill = 16;  // persistent kernels only
+    if (const char *r = std::getenv("PUPIL_REFILL")) sc.trace_refill = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     if (const char *po = std::getenv("PUPIL_PRIMARY_ORDER")) pt->primary_interleave = std::strcmp(po, "path") != 0;
     {  // one material bin in the whole scene: the material partition orders nothing (auto; =bins / =list force)
         uint32_t bins = 0;
@@ -919,15 +845,13 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
         sc.single_bin = pt->shade_list && bins && (bins & (bins - 1u)) == 0u ? (uint32_t)__builtin_ctz(bins) : 0u;
     }
     if (const char *fr = std::getenv("PUPIL_FRESH_SHADE")) pt->fresh_shade = std::atoi(fr) != 0;
-    pt->mixed_trace = true;
-    if (const char *m = std::getenv("PUPIL_MIXED")) pt->mixed_trace = std::atoi(m) != 0;
     if (const char *a = std::getenv("PUPIL_AHEAD")) pt->ahead_mode = std::min(2, std::max(0, std::atoi(a)));
     if (const char *k = std::getenv("PUPIL_PIPE")) pt->pipe_limit = (uint32_t)std::min(63, std::max(0, std::atoi(k)));
     if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
     if (const char *g = std::getenv("PUPIL_PIPE_PATHS")) pt->pipe_paths = std::max(1.0, std::atof(g));
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
-    if (sc.bvh_width == 4 && nodes4_count(pt) > kMaxNodes4)
+    if (nodes4_count(pt) > kMaxNodes4)
         return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "BVH4 larger than 2^26 nodes (32-bit node offsets)"));
     sc.prim_inst = d_prim_inst;
     sc.instances = d_insts;
@@ -946,12 +870,9 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
     if (refresh_node_bound(pt) != PUPIL_OK) return cleanup(PUPIL_ERR_HIP);
-    pt->totals.bvh_nodes = pt->two_level ? two_level_nodes(pt->tl)
-                           : (pt->sc.bvh_width == 8 ? pt->bvh.num_nodes8
-                                                    : (pt->sc.bvh_width == 4 ? pt->bvh.num_nodes4 : pt->bvh.num_nodes));
+    pt->totals.bvh_nodes = pt->two_level ? two_level_nodes(pt->tl) : pt->bvh.num_nodes4;
     pt->totals.two_level = pt->two_level ? 1u : 0u;
-    pt->totals.bvh_depth = pt->two_level ? pt->tl.tlas_depth + pt->tl.blas_depth
-                                         : (pt->sc.bvh_width == 8 ? pt->bvh.depth8 : pt->bvh.depth4);
+    pt->totals.bvh_depth = pt->two_level ? pt->tl.tlas_depth + pt->tl.blas_depth : pt->bvh.depth4;
     pt->totals.bvh_prims = pt->num_prims;
     pt->totals.build_ms = pt->build_ms;
     *out = pt;
@@ -999,10 +920,9 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
         return PUPIL_OK;
     }
     BvhBuildInput bin{pt->num_prims, pt->d_prim_inst, pt->d_insts, pt->d_mats};
-    bin.wide8 = pt->sc.bvh_width == 8 ? 1u : 0u;
-    // refit in place (PUPIL_FLAT_UPDATE=rebuild, or the BVH2 / BVH8 node formats: full rebuild)
+    // refit in place (PUPIL_FLAT_UPDATE=rebuild: full rebuild)
     const char *fu = std::getenv("PUPIL_FLAT_UPDATE");
-    if (pt->sc.bvh_width == 4 && !(fu && std::strcmp(fu, "rebuild") == 0)) {
+    if (!(fu && std::strcmp(fu, "rebuild") == 0)) {
         double rms = 0.0;
         if (refit_bvh4(bin, pt->bvh, instance, pt->own_stream, &rms) == 0) {
             pt->totals.build_ms = rms;
@@ -1019,16 +939,12 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     }
     free_lbvh(pt->bvh);
     pt->bvh = nb;
-    pt->sc.nodes = nb.nodes;
     pt->sc.prims = nb.prims;
     pt->sc.attrs = nb.attrs;
-    pt->sc.root_link = nb.root_link;
     pt->sc.nodes4 = nb.nodes4;
     pt->sc.root_link4 = nb.root_link4;
-    pt->sc.nodes8 = nb.nodes8;
-    pt->sc.root_link8 = nb.root_link8;
-    pt->totals.bvh_nodes = pt->sc.bvh_width == 8 ? nb.num_nodes8 : (pt->sc.bvh_width == 4 ? nb.num_nodes4 : nb.num_nodes);
-    pt->totals.bvh_depth = pt->sc.bvh_width == 8 ? nb.depth8 : nb.depth4;
+    pt->totals.bvh_nodes = nb.num_nodes4;
+    pt->totals.bvh_depth = nb.depth4;
     pt->totals.build_ms = ms;
     return refresh_node_bound(pt);
 }
@@ -1142,11 +1058,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
 
     HIP_TRY(hipEventRecord(pt->ev_begin, s));
     if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 32 * sizeof(unsigned long long), s));
-    // the persistent BVH4 kernels with mixed extension + shadow launches pipeline frames;
-    // the A/B traversal variants (BVH2 / BVH8 node formats, one ray per lane, separate
-    // shadow and extension launches) render each batch on its own
-    const bool pipelined = pt->mixed_trace && pt->sc.bvh_width == 4 && pt->sc.trace_refill != 0;
-    const int rc = pipelined ? render_pipelined(cx, fp, launch) : render_classic(cx, fp);
+    const int rc = render_pipelined(cx, fp, launch);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(pt->ev_end, s));
     HIP_TRY(hipGetLastError());
@@ -1269,7 +1181,7 @@ void pupil_pt_destroy(pupil_pt *pt) { delete pt; }
 int pupil_pt_export_bvh4(pupil_pt *pt, uint32_t *num_nodes, void *nodes, uint32_t *num_records, float *records,
                          int32_t *root_link) {
     if (!pt || !num_nodes || !num_records || !root_link) return fail(PUPIL_ERR_INVALID, "null argument");
-    if (pt->two_level || pt->sc.bvh_width != 4) return fail(PUPIL_ERR_UNSUPPORTED, "only the flattened BVH4 is exported");
+    if (pt->two_level) return fail(PUPIL_ERR_UNSUPPORTED, "only the flattened BVH4 is exported");
     HIP_TRY(hipSetDevice(pt->device));
     const uint32_t nn = pt->bvh.num_nodes4, nr = pt->bvh.num_records;
     if (nodes || records) {

@@ -15,23 +15,14 @@ constexpr int kTraceBlock = 128;
 #define PUPIL_W4_WAVES 7
 #endif
 constexpr int kTraceWavesPerSimd = PUPIL_W4_WAVES;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8 waves at <= 64 VGPRs: 11 % slower, r03 A/B)
-#ifndef PUPIL_W8_WAVES  // A/B builds only (tools/dbg: the spilled 6-wave BVH8 kernels)
-#define PUPIL_W8_WAVES 5
-#endif
-constexpr int kTraceWavesPerSimd8 = PUPIL_W8_WAVES;  // BVH8 kernels (<= 96 VGPRs; 6 waves spill 17 registers: 24.2 vs 23.7 ms)
 constexpr int kTraceWavesPerSimdTL = 5;  // two-level variant (<= 96 VGPRs; A/B r02 on config 5: 4 waves 688, 5: 743, 6: 716 Mrays/s)
-constexpr int kStackLds = 32;   // per-thread LDS stack entries
 constexpr int kStackOvf = 160;  // per-thread global overflow entries
 constexpr int kRing = 16;       // persistent BVH4 kernels: per-lane LDS ring entries (spills to the overflow column)
 // Stack entries a traversal may need: 3 per BVH4 level (4 children, one taken), plus
 // 2 per instance entry in two-level mode.  Builds whose trees need more are rejected
 // (or rebuilt with the depth-bounded Karras LBVH) at create time, so no kernel ever
 // overwrites a live entry.
-constexpr int kTraceStackEntries = kRing + kStackOvf < kStackLds + kStackOvf ? kRing + kStackOvf : kStackLds + kStackOvf;
-// BVH8 kernels: stack entries are (base, bits) pairs: kRing8 in the LDS ring, the
-// overflow column's kStackOvf ints hold kStackOvf / 2 more
-constexpr int kRing8 = 8;
-constexpr int kTrace8StackEntries = kRing8 + kStackOvf / 2;
+constexpr int kTraceStackEntries = kRing + kStackOvf;
 constexpr int kShadeBlock = 256;
 constexpr uint32_t kMaxDepth = 128;  // PTPass inspector range (pt_pass.cpp:225-237)
 constexpr uint32_t kNumQueues = 9;  // 0 = miss, 1..7 = EMatType, 8 = unknown material
@@ -195,8 +186,6 @@ enum ShadeList : int { kShadeBins = 0, kShadeAll = 1, kShadeNext = 2, kShadeNext
 void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, const Queues &q, uint32_t tag,
                   hipStream_t s, ShadeList list, uint32_t range_base, uint32_t range_n, uint32_t max_count,
                   bool fresh_range = false, uint32_t fresh_seed0 = 0);
-void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
-                   const TraceStats *stats, hipStream_t s);
 // one persistent launch over the next + shadow lists of a bounce (BVH4 persistent path only)
 // ahead_count > 0 (render-ahead, BVH4 kernels only): the launch also traces the camera
 // rays of the next render.  `ps` is then the base of both buffer halves: this render's
@@ -237,23 +226,15 @@ struct BvhBuildInput {
     const DevInstance *instances;   // device
     const DevMaterial *materials;   // device
     uint32_t object_space;          // 1: BLAS build (vertices untransformed, shading records in primitive order)
-    uint32_t wide8 = 0;             // 1: collapse to the 8-wide Bvh8Node tree instead of the BVH4 (flat scenes)
 };
 struct BvhBuildOutput {
-    BvhNode *nodes;     // device, max(1, n-1)
-    Bvh4Node *nodes4;   // device, collapsed 4-wide quantized tree (null for wide8 builds)
-    Bvh8Node *nodes8;   // device, wide8 builds: 8-wide tree; records at kLeafSlots * node + slot
+    Bvh4Node *nodes4;   // device, collapsed 4-wide quantized tree
     float4 *prims;      // device, 3 * n
     float4 *attrs;      // device, kAttrStride * n shading records (same order)
-    uint32_t root_link;
-    uint32_t root_link4;
-    uint32_t num_nodes;
+    uint32_t root_link4;      // link of the root (internal 0 or a leaf)
     uint32_t num_nodes4;
     uint32_t depth4;    // levels of the BVH4 (1 = root only); 0 = not measured (A/B collapse)
-    uint32_t num_nodes8 = 0;
-    uint32_t depth8 = 0;      // levels of the BVH8
-    uint32_t root_link8 = 0;
-    uint32_t num_records = 0; // primitive records (wide8: kLeafSlots per node, with holes)
+    uint32_t num_records = 0; // primitive records
     // first node of each BVH4 level (breadth-first collapse order) and the end; empty when
     // not measured.  Children always lie on a later level (bottom-up refits walk it backwards).
     std::vector<uint32_t> level_start;

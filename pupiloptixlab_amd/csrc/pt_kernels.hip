@@ -16,7 +16,6 @@
 // Every float operation of the reference is reproduced in the same order, so
 // a path gives bit-identical radiance to the reference-order CPU oracle.
 #include "pt_kernels.h"
-#include "pt_kernels_alt.h"
 #include "pt_shading.h"
 #include "pt_trace.h"
 #include "pt_traverse.h"
@@ -66,11 +65,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     const uint32_t n_next = kMixed ? q.counts[kCntNext] : 0u;
     // mixed launches may carry the next render's camera rays (render-ahead, TraceJob::ahead_off)
     const uint32_t n_ahead = MODE == kModeMixedAhead ? job.static_count : 0u;
-    const uint32_t count =
-        MODE == kModeShadow ? q.counts[kCntShadow]
-                            : (kMixed ? n_next + q.counts[kCntShadow]
-                                                  : (job.count_ptr ? *job.count_ptr : job.static_count));
-    const uint32_t *shadow_q = MODE == kModeShadow ? q.nxsh + q.counts[kStartShadow] : nullptr;
+    const uint32_t count = kMixed ? n_next + q.counts[kCntShadow] : (job.count_ptr ? *job.count_ptr : job.static_count);
     RingStack st;
     st.lds = s_ring + threadIdx.x;
     st.ovf = ovf + blockIdx.x * blockDim.x + threadIdx.x;
@@ -160,12 +155,6 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         d = ld_ps(ps.ray_d + p);
                         tmin = 0.001f;
                         tmax = kMaxDistance;
-                    } else if (MODE == kModeShadow) {
-                        p = shadow_q[i];
-                        o = ld_ps(ps.ray_o + p);  // shadow rays share the origin record, w = tmax
-                        d = ld_ps(ps.sh_d + p);
-                        tmin = 0.001f;
-                        tmax = o.w;
                     } else if (MODE == kModeMixedAhead && k < len_a) {
                         // a camera ray of the next render (generated into the other half of the
                         // path state): the primary extend's pixel-major dequeue, then the offset
@@ -346,8 +335,8 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 if (sc.single_bin == 0u) ps.mbin[p] = (uint8_t)bin;  // material bin for the partition
             }
         }
-        if (MODE == kModeShadow || kMixed) {
-            if (done && any && !found) {  // main.cu:124-139
+        if (kMixed) {
+            if (done && any && !found) {  // main.cu:124-139 (shadow rays share the origin record, w = tmax)
                 const float4 c = ld_ps(ps.sh_c + p);
                 float4 L = ld_ps(ps.rad + p);
                 L.x = L.x + c.x;
@@ -365,7 +354,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         if (STATS) q_ret += (uint32_t)__popcll(__ballot(done));
         if (done) active = false;
     }
-    flush_stats<STATS>(&stats, nv, npt, MODE == kModeShadow ? 14 : 0);
+    flush_stats<STATS>(&stats, nv, npt, 0);
     if (kMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
     flush_stats<STATS>(&stats, n_unique, 0u, 18);
     if (STATS && stats.wave_times && lane_id() == 0) {
@@ -402,7 +391,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             dg[k] = v;
         }
         if (lane_id() == 0)
-            for (int k = 0; k < 6; k++) atomicAdd(&stats.counters[(MODE == kModeShadow ? 8 : 2) + k], dg[k]);
+            for (int k = 0; k < 6; k++) atomicAdd(&stats.counters[2 + k], dg[k]);
     }
 }
 
@@ -909,8 +898,7 @@ uint32_t trace4_blocks(const DeviceScene &sc, uint32_t ovf_threads) {
         const char *e = std::getenv("PUPIL_TRACE_GRID_WAVES");
         return e ? std::max(1, std::atoi(e)) : 0;
     }();
-    const uint32_t occ = sc.bvh_width == 8 ? kTraceWavesPerSimd8
-                         : (sc.two_level && !sc.tl_world ? kTraceWavesPerSimdTL : kTraceWavesPerSimd);
+    const uint32_t occ = sc.two_level && !sc.tl_world ? kTraceWavesPerSimdTL : kTraceWavesPerSimd;
     const uint32_t waves = forced ? std::min(occ, (uint32_t)forced) : occ;
     const uint32_t resident = sc.num_cus * 4u * waves / (kTraceBlock / 64u);
     return std::min(ovf_threads / kTraceBlock, std::max(1u, resident));
@@ -922,9 +910,7 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
                           uint32_t ovf_threads, const TraceStats *stats, hipStream_t s) {
     const TraceStats st = stats ? *stats : TraceStats{nullptr};
     const uint32_t blocks = trace4_blocks(sc, ovf_threads);
-    if (sc.bvh_width == 8) {
-        launch_trace8(MODE, ANY, sc, ps, q, job, ovf, ovf_threads, stats, s);  // pt_kernels_alt.hip
-    } else if (sc.two_level && !sc.tl_world) {
+    if (sc.two_level && !sc.tl_world) {
         if (stats)
             hipLaunchKernelGGL((k_trace4tl<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
                                ovf, ovf_threads, st);
@@ -942,16 +928,13 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
 
 void launch_trace_debug(const DeviceScene &sc, const float *rays, float *out, uint32_t n, int any, int *ovf,
                         uint32_t ovf_threads, uint32_t *work, hipStream_t s, const TraceStats *stats) {
-    if ((sc.bvh_width == 4 || sc.bvh_width == 8) && sc.trace_refill) {  // the production kernel, fed from a ray array
-        const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, sc.trace_node_min, rays, out, 0u, 0u};
-        const Queues q{};
-        if (any)
-            launch_trace4<kModeRays, true>(sc, PathState{}, q, job, ovf, ovf_threads, stats, s);
-        else
-            launch_trace4<kModeRays, false>(sc, PathState{}, q, job, ovf, ovf_threads, stats, s);
-        return;
-    }
-    launch_trace_debug_lanes(sc, rays, out, n, any, ovf, ovf_threads, s);
+    // the production kernel, fed from a ray array
+    const TraceJob job{nullptr, nullptr, n, work, sc.trace_refill, sc.trace_node_min, rays, out, 0u, 0u};
+    const Queues q{};
+    if (any)
+        launch_trace4<kModeRays, true>(sc, PathState{}, q, job, ovf, ovf_threads, stats, s);
+    else
+        launch_trace4<kModeRays, false>(sc, PathState{}, q, job, ovf, ovf_threads, stats, s);
 }
 
 __global__ void k_debug_select(DeviceScene sc, const float *p, int *out, uint32_t n) {
@@ -981,23 +964,9 @@ void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathSta
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
                    const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
                    const TraceStats *stats, hipStream_t s, uint32_t interleave_spp, uint32_t num_local) {
-    if ((sc.bvh_width == 4 || sc.bvh_width == 8) && sc.trace_refill) {
-        const TraceJob job{queue,   queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min,
-                           nullptr, nullptr,     queue ? 0u : interleave_spp, num_local};
-        launch_trace4<kModeExtend, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
-        return;
-    }
-    launch_extend_lanes(sc, ps, q, queue, queue_count, static_count, ovf, ovf_threads, stats, s);
-}
-
-void launch_shadow(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
-                   const TraceStats *stats, hipStream_t s) {
-    if ((sc.bvh_width == 4 || sc.bvh_width == 8) && sc.trace_refill) {
-        const TraceJob job{nullptr, nullptr, 0u, q.work + kWorkShadow, sc.trace_refill, sc.trace_node_min, nullptr, nullptr, 0u, 0u};
-        launch_trace4<kModeShadow, true>(sc, ps, q, job, ovf, ovf_threads, stats, s);
-        return;
-    }
-    launch_shadow_lanes(sc, ps, q, ovf, ovf_threads, stats, s);
+    const TraceJob job{queue,   queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min,
+                       nullptr, nullptr,     queue ? 0u : interleave_spp, num_local};
+    launch_trace4<kModeExtend, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
 }
 
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,

@@ -2,10 +2,10 @@
 //
 // Everything the wavefront kernels read lives in one POD struct (DeviceScene)
 // passed by value as a kernel argument.  Layout choices (HBM-first):
-//   * BVH nodes: 64 B BVH2 nodes (two child boxes + two child links), 64 B
-//     aligned so one node = one half L2 line; leaves index a Morton-ordered
-//     array of 48 B primitive records (3 x float4: world-space triangle
-//     vertices; the first w carries the global primitive id).
+//   * BVH nodes: 64 B quantized 4-wide nodes (Bvh4Node), 64 B aligned so one
+//     node = one half L2 line; leaves index a Morton-ordered array of 48 B
+//     primitive records (3 x float4: world-space triangle vertices; the first w
+//     carries the global primitive id).
 //   * Shading data stays in object space and is gathered only on hits
 //     (reference: geometry.h:48-96 interpolates object-space attributes then
 //     transforms), so the traversal working set is nodes + prim records only.
@@ -91,13 +91,6 @@ struct DevInstance {
     float vmax;  // largest |object-space vertex coordinate| of the shape (margins)
 };
 
-struct alignas(16) BvhNode {
-    float4 lo0;  // xyz = child0 min, w = child0 link (int bits)
-    float4 hi0;  // xyz = child0 max, w = child1 link
-    float4 lo1;  // xyz = child1 min
-    float4 hi1;  // xyz = child1 max
-};
-
 // 4-wide node with 8-bit quantized child boxes: 64 B = one half L2 line holds
 // what four 64 B BVH2 nodes spread over two levels.  Child k's box is
 // origin + q * s per axis, s a power of two stored as a float (r03: the traversal
@@ -112,24 +105,6 @@ struct alignas(64) Bvh4Node {
     uint32_t qhi_x, qhi_y, qhi_z;
     float sy, sz;       // scales of the y and z planes
 };
-// 8-wide node (PUPIL_BVH_WIDTH=8, flattened BVH): one 128-B line, 80 B read.
-// Child slot k: box quantized like Bvh4Node (planes in byte k % 4 of word k / 4);
-// internal children (imask bit k) are nodes child_base + (internal slots below k),
-// so a stack entry is a whole node group (child_base, slot hit bits, imask); a leaf
-// child in slot k holds up to 2 primitives, records kLeafSlots * node + 2k + {0, 1}
-// (pvalid bit 2k + j: record present).  Slots are assigned by the child's centroid
-// offset octant (Ylitie et al. 2017), so slot k ^ octant(ray) orders a node's
-// children roughly front to back.
-struct alignas(128) Bvh8Node {
-    float ox, oy, oz;
-    uint32_t exps;        // e_x | e_y << 8 | e_z << 16 | imask << 24
-    uint32_t child_base;  // first internal child node
-    uint32_t pvalid;      // bits 0..15: record slots holding a primitive
-    uint32_t pad0[2];
-    uint32_t qlo_x[2], qhi_x[2], qlo_y[2], qhi_y[2], qlo_z[2], qhi_z[2];
-    uint32_t pad1[12];
-};
-constexpr uint32_t kLeafSlots = 16;  // primitive record slots per Bvh8Node
 constexpr int kEmptyLink = 0x7FFFFFFF;
 // Largest BVH4 node array: the traversal addresses nodes by 32-bit byte offsets.
 constexpr uint64_t kMaxNodes4 = 1ull << 26;
@@ -156,16 +131,11 @@ struct Camera {
 };
 
 struct DeviceScene {
-    const BvhNode *nodes;
     const Bvh4Node *nodes4;
-    const Bvh8Node *nodes8;  // bvh_width 8: records at kLeafSlots * node + slot
     const float4 *prims;  // 3 float4 per primitive, Morton order
     const float4 *attrs;  // kAttrStride float4 per primitive, same order (hit reconstruction)
     uint32_t num_prims;
-    uint32_t root_link;   // link of the root (internal 0 or a leaf), BVH2
-    uint32_t root_link4;  // same for the BVH4
-    uint32_t root_link8;  // BVH8: 0 = node 0, a leaf link = records [0, n), kTraverseDone = empty
-    uint32_t bvh_width;   // 2, 4 or 8: which node array the traversal kernels use
+    uint32_t root_link4;  // link of the root (internal 0 or a leaf), kTraverseDone = empty
     uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
     uint32_t num_cus;       // compute units of the device (persistent grid size)
     uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node

@@ -1,8 +1,7 @@
-// pt_traverse.h — device code shared by the traversal kernels of pt_kernels.hip
-// (the production persistent BVH4 kernels) and pt_kernels_alt.hip (the A/B
-// families: one-ray-per-lane BVH2 / BVH4 kernels, the persistent BVH8 kernels,
-// the ray-query verification kernel): stacks, leaf tests, the persistent-kernel
-// job descriptor and the quantized BVH4 box test.
+// pt_traverse.h — device code of the persistent BVH4 traversal kernels
+// (pt_kernels.hip: path tracing launches and the ray-query verification launch):
+// leaf tests, the LDS ring stack, the persistent-kernel job descriptor and the
+// quantized BVH4 box test.
 #pragma once
 
 #include "pt_kernels.h"
@@ -12,6 +11,7 @@
 namespace pupil {
 namespace tr {
 
+constexpr int kSentinel = kTraverseDone;
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
@@ -19,123 +19,7 @@ __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << la
 __device__ __forceinline__ vec3 f3(float4 v) { return v3(v.x, v.y, v.z); }
 __device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
-// ------------------------------------------------------------------ traversal
-// Stack: kStackLds entries in LDS (lane-interleaved), overflow to HBM.
-struct Stack {
-    int *lds;          // this thread's column base
-    int *ovf;          // this thread's overflow base
-    uint32_t ovf_stride;
-    // indices are clamped to the capacity: a pathological tree can only give
-    // a wrong answer, never an out-of-bounds access
-    __device__ __forceinline__ void store(int i, int v) {
-        i = min(i, kStackLds + kStackOvf - 1);
-        if (i < kStackLds) lds[i * kTraceBlock] = v;
-        else ovf[(size_t)(i - kStackLds) * ovf_stride] = v;
-    }
-    __device__ __forceinline__ int load(int i) const {
-        i = max(0, min(i, kStackLds + kStackOvf - 1));
-        return i < kStackLds ? lds[i * kTraceBlock] : ovf[(size_t)(i - kStackLds) * ovf_stride];
-    }
-};
-
-constexpr int kSentinel = kTraverseDone;
-
-// Aila-Laine while-while traversal with postponed leaves.  ANY = shadow
-// (terminate on first hit, OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT).
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool traverse(const DeviceScene &sc, const RayPre &r, float tmin, float &tmax,
-                                         uint32_t &best_key, uint32_t &best_idx, float &bb1, float &bb2, Stack &st,
-                                         uint32_t &nodes_visited, uint32_t &prims_tested) {
-    int sp = 0;
-    st.store(0, kSentinel);
-    int node = (int)sc.root_link;
-    int leaf = 0;
-    if (node < 0) {  // the whole scene is one leaf
-        leaf = node;
-        node = kSentinel;
-    }
-    bool found = false;
-    while (node != kSentinel || leaf < 0) {
-        while ((uint32_t)node < (uint32_t)kSentinel) {
-            const BvhNode n = sc.nodes[node];
-            if (STATS) nodes_visited++;
-            const float t0 = box_entry(r, v3(n.lo0.x, n.lo0.y, n.lo0.z), v3(n.hi0.x, n.hi0.y, n.hi0.z), tmin, tmax);
-            const float t1 = box_entry(r, v3(n.lo1.x, n.lo1.y, n.lo1.z), v3(n.hi1.x, n.hi1.y, n.hi1.z), tmin, tmax);
-            const bool h0 = t0 != __builtin_huge_valf();
-            const bool h1 = t1 != __builtin_huge_valf();
-            int c0 = __float_as_int(n.lo0.w);
-            int c1 = __float_as_int(n.hi0.w);
-            if (!h0 && !h1) {
-                node = st.load(sp);
-                sp--;
-            } else {
-                node = h0 ? c0 : c1;
-                if (h0 && h1) {
-                    if (t1 < t0) {
-                        const int tmp = node;
-                        node = c1;
-                        c1 = tmp;
-                    }
-                    sp++;
-                    if (sp >= kStackLds + kStackOvf) sp = kStackLds + kStackOvf - 1;  // never reached (depth <= 62)
-                    st.store(sp, c1);
-                }
-            }
-            if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
-                leaf = node;
-                node = st.load(sp);
-                sp--;
-            }
-            if (!__any(leaf >= 0)) break;
-        }
-        while (leaf < 0) {
-            const uint32_t first = leaf_first(leaf);
-            const uint32_t count = leaf_count(leaf);
-            for (uint32_t i = first; i < first + count; i++) {
-                const float4 a = sc.prims[3 * i + 0];
-                const uint32_t ref = __float_as_uint(a.w);
-                const uint32_t key = ref & ~kPrimSphereBit;
-                if (STATS) prims_tested++;
-                float t, b1 = 0.f, b2 = 0.f;
-                bool hit;
-                if (ref & kPrimSphereBit) {
-                    const float4 b = sc.prims[3 * i + 1];
-                    const DevInstance &in = sc.instances[__float_as_uint(b.w)];
-                    hit = intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, t);
-                } else {
-                    const float4 b = sc.prims[3 * i + 1];
-                    const float4 c = sc.prims[3 * i + 2];
-                    hit = intersect_triangle(r, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), tmin, tmax, t,
-                                             b1, b2);
-                }
-                if (hit) {
-                    if (ANY) {
-                        found = true;
-                        break;
-                    }
-                    if (t < tmax || key < best_key) {
-                        tmax = t;
-                        best_key = key;
-                        best_idx = i;
-                        bb1 = b1;
-                        bb2 = b2;
-                        found = true;
-                    }
-                }
-            }
-            if (ANY && found) break;
-            leaf = node;
-            if (node < 0) {
-                node = st.load(sp);
-                sp--;
-            }
-        }
-        if (ANY && found) break;
-    }
-    return found;
-}
-
-// Leaf intersection shared by both node formats.  any = terminate on the first
+// Leaf intersection (flattened BVH4 and two-level world mode).  any = terminate on the first
 // hit (shadow ray); a compile-time constant except in the mixed persistent kernel.
 template <bool STATS>
 __device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
@@ -217,103 +101,6 @@ __device__ __forceinline__ bool intersect_leaf_tl(const DeviceScene &sc, const R
         }
     }
     return false;
-}
-
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool intersect_leaf(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
-                                               float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
-                                               float &bb2, uint32_t &prims_tested, bool &found) {
-    return intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, bb1, bb2, prims_tested, found, ANY);
-}
-
-__device__ __forceinline__ void cswap(float &ta, int &la, float &tb, int &lb) {
-    if (tb < ta) {
-        const float t = ta;
-        ta = tb;
-        tb = t;
-        const int l = la;
-        la = lb;
-        lb = l;
-    }
-}
-
-// 4-wide quantized traversal (same while-while / postponed-leaf structure).
-// Child boxes are decoded exactly as the builder verified them, then slab-
-// tested with the conservative test; hits are sorted near-to-far with a
-// 5-comparator network, the nearest is descended, the rest pushed.
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool traverse4(const DeviceScene &sc, const RayPre &r, float tmin, float &tmax,
-                                          uint32_t &best_key, uint32_t &best_idx, float &bb1, float &bb2, Stack &st,
-                                          uint32_t &nodes_visited, uint32_t &prims_tested) {
-    constexpr float kInf = __builtin_huge_valf();
-    int sp = 0;
-    st.store(0, kSentinel);
-    int node = (int)sc.root_link4;
-    int leaf = 0;
-    if (node < 0) {  // the whole scene is one leaf
-        leaf = node;
-        node = kSentinel;
-    }
-    bool found = false;
-    while (node != kSentinel || leaf < 0) {
-        while ((uint32_t)node < (uint32_t)kSentinel) {
-            const Bvh4Node n = sc.nodes4[node];
-            if (STATS) nodes_visited++;
-            const float sx = n.sx, sy = n.sy, sz = n.sz;
-            float t[4];
-            int l[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const vec3 lo = v3(n.ox + (float)((n.qlo_x >> (8 * k)) & 0xFFu) * sx,
-                                   n.oy + (float)((n.qlo_y >> (8 * k)) & 0xFFu) * sy,
-                                   n.oz + (float)((n.qlo_z >> (8 * k)) & 0xFFu) * sz);
-                const vec3 hi = v3(n.ox + (float)((n.qhi_x >> (8 * k)) & 0xFFu) * sx,
-                                   n.oy + (float)((n.qhi_y >> (8 * k)) & 0xFFu) * sy,
-                                   n.oz + (float)((n.qhi_z >> (8 * k)) & 0xFFu) * sz);
-                l[k] = n.child[k];
-                const float te = box_entry(r, lo, hi, tmin, tmax);
-                t[k] = l[k] != kEmptyLink ? te : kInf;
-            }
-            cswap(t[0], l[0], t[1], l[1]);
-            cswap(t[2], l[2], t[3], l[3]);
-            cswap(t[0], l[0], t[2], l[2]);
-            cswap(t[1], l[1], t[3], l[3]);
-            cswap(t[1], l[1], t[2], l[2]);
-            if (t[0] == kInf) {
-                node = st.load(sp);
-                sp--;
-            } else {
-                node = l[0];
-                if (t[3] != kInf) st.store(++sp, l[3]);
-                if (t[2] != kInf) st.store(++sp, l[2]);
-                if (t[1] != kInf) st.store(++sp, l[1]);
-            }
-            if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
-                leaf = node;
-                node = st.load(sp);
-                sp--;
-            }
-            if (!__any(leaf >= 0)) break;
-        }
-        while (leaf < 0) {
-            if (intersect_leaf<ANY, STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, bb1, bb2, prims_tested, found))
-                return true;
-            leaf = node;
-            if (node < 0) {
-                node = st.load(sp);
-                sp--;
-            }
-        }
-    }
-    return found;
-}
-
-template <bool ANY, bool STATS, int W>
-__device__ __forceinline__ bool trace_ray(const DeviceScene &sc, const RayPre &r, float tmin, float &tmax,
-                                          uint32_t &best_key, uint32_t &best_idx, float &bb1, float &bb2, Stack &st,
-                                          uint32_t &nv, uint32_t &pt) {
-    if constexpr (W == 4) return traverse4<ANY, STATS>(sc, r, tmin, tmax, best_key, best_idx, bb1, bb2, st, nv, pt);
-    else return traverse<ANY, STATS>(sc, r, tmin, tmax, best_key, best_idx, bb1, bb2, st, nv, pt);
 }
 
 // counters[0..1]: closest-hit (extend / ray queries), counters[14..15]: shadow
@@ -402,7 +189,8 @@ __device__ __forceinline__ void csel(float &ta, int &la, float &tb, int &lb) {
 // bounce pays one persistent-kernel tail instead of two.
 // kModeMixedAhead: kModeMixed plus the next render's camera rays (render-ahead,
 // TraceJob::ahead_off); a separate instance so the plain mixed kernel keeps its registers
-enum TraceMode : int { kModeExtend = 0, kModeShadow = 1, kModeRays = 2, kModeMixed = 3, kModeMixedAhead = 4 };
+// (value 1, the separate any-hit launch of r01, is retired; the numbers name the kernel instances)
+enum TraceMode : int { kModeExtend = 0, kModeRays = 2, kModeMixed = 3, kModeMixedAhead = 4 };
 
 struct TraceJob {
     const uint32_t *queue;      // extend: path ids (null = identity)

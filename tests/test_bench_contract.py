@@ -74,3 +74,58 @@ def test_roofline_rank_of_an_8_way_shard_stays_below_one(monkeypatch):
         assert 0 < v["frac"] <= 1, (k, v["frac"])
         assert v["frac"] < one["ceilings"][k]["frac"]  # the same work per ray, less of it per second
     assert abs(rank["traffic"] - one["traffic"] / 8) < 1e3
+
+
+# ---------------------------------------------------------------- launcher (--gpus N)
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")):
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(HERE, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=300, env=env)
+
+
+def test_plain_bench_gpus_2_spawns_two_ranks():
+    """`python bench.py --gpus 2` with no launcher starts two rank processes (fresh
+    interpreters, torchrun's environment) that form one group; rank 0 reports both."""
+    r = _run(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["ranks_seen"] == 2 and rec["gpus_requested"] == 2
+    assert os.getpid() not in rec["pids"] and len(set(rec["pids"])) == 2
+
+
+def test_bench_gpus_3_spawns_three_ranks():
+    r = _run(["--gpus", "3", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["n_gpus"] == 3 and rec["ranks_seen"] == 3
+
+
+def test_bench_world_size_disagreeing_with_gpus_fails():
+    """Under a launcher, WORLD_SIZE must equal --gpus: a mismatch exits non-zero
+    instead of printing an n_gpus the driver did not ask for."""
+    r = _run(["--gpus", "1", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+    r = _run(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0
+
+
+def test_failing_rank_fails_the_launch():
+    """A rank that dies makes the whole launch fail and stops the rank still waiting
+    for it in the rendezvous (no hang)."""
+    import time
+
+    t0 = time.time()
+    r = _run(["--gpus", "2", "--dry-run"], {"PUPIL_BENCH_DRY_FAIL_RANK": "1"})
+    assert r.returncode == 3 and time.time() - t0 < 120
+    assert _run(["--gpus", "2", "--dry-run", "--config", "9"]).returncode != 0  # bad arguments

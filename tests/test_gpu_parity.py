@@ -77,9 +77,9 @@ def _cornell(res, depth=4):
     return World().load_scene(scenes.cornell_xml(os.path.join(TMP, f"cb{res}.xml"), res, res, depth))
 
 
-@pytest.mark.parametrize("width", ["2", "4", "8"])
-def test_primary_hits_match_oracle(width, monkeypatch):
-    monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+@pytest.mark.parametrize("refill", ["1", "16", "64"])
+def test_primary_hits_match_oracle(refill, monkeypatch):
+    monkeypatch.setenv("PUPIL_REFILL", refill)
     w = _cornell(96)
     desc = w.desc()
     o = oracle.OracleScene(desc)
@@ -149,13 +149,10 @@ def test_config1_cornellbox_named_size():
     assert rs["shadow_rays"] <= rs["shadow_rays_reference"] <= rs["primary_rays"] * (d.max_depth - 1)
 
 
-@pytest.mark.parametrize("accel", ["flat", "flat8", "two_level"])
+@pytest.mark.parametrize("accel", ["flat", "two_level"])
 def test_materials_parity_config2(accel, monkeypatch):
     """Config 2 (all seven BSDFs, spheres + boxes) at 192^2, 8 spp, depth 6; one flattened
-    BVH (BVH4 or BVH8 nodes), or a TLAS over the mesh and sphere instances."""
-    if accel == "flat8":
-        monkeypatch.setenv("PUPIL_BVH_WIDTH", "8")
-        accel = "flat"
+    BVH4, or a TLAS over the mesh and sphere instances."""
     monkeypatch.setenv("PUPIL_ACCEL", accel)
     p = scenes.cornell_materials_xml(os.path.join(TMP, "cbmat.xml"), 192, 192, 6)
     desc = World().load_scene(p).desc()
@@ -165,24 +162,25 @@ def test_materials_parity_config2(accel, monkeypatch):
     assert compare(gpu, ref, f"materials192x8-{accel}") == 192 * 192
 
 
-@pytest.mark.parametrize("width", ["2", "4", "8"])
-def test_sphere_field_parity(width, monkeypatch):
-    monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+@pytest.mark.parametrize("refill", ["1", "16", "64"])
+def test_sphere_field_parity(refill, monkeypatch):
+    monkeypatch.setenv("PUPIL_REFILL", refill)
     w = scenes.sphere_field(27, 240, 136, 4, seed=3)
     desc = w.desc()
     gpu = render_gpu(desc, 2)
     ref = oracle.OracleScene(desc).render(spp=2)
-    compare(gpu, ref, f"field27-bvh{width}")
+    compare(gpu, ref, f"field27-refill{refill}")
 
 
-@pytest.mark.parametrize("mixed", ["0", "1"])
-def test_stage_schedules_parity(mixed, monkeypatch):
-    """Separate shadow and extension launches per bounce, or one mixed launch over both lists."""
-    monkeypatch.setenv("PUPIL_MIXED", mixed)
+@pytest.mark.parametrize("node_min", ["1", "8", "64"])
+def test_stage_schedules_parity(node_min, monkeypatch):
+    """The mixed extension + shadow launch with the node phase left at 1, 8 (default) or 64
+    active lanes: lanes switch between node and leaf phases at other points, hits do not change."""
+    monkeypatch.setenv("PUPIL_NODE_MIN", node_min)
     desc = scenes.sphere_field(27, 200, 120, 5, seed=4).desc()
     gpu = render_gpu(desc, 3)
     ref = oracle.OracleScene(desc).render(spp=3)
-    exact = compare(gpu, ref, f"schedule-mixed{mixed}")
+    exact = compare(gpu, ref, f"schedule-node_min{node_min}")
     assert exact == 200 * 120
     s, rs = gpu["stats"], ref["stats"]
     assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
@@ -200,8 +198,9 @@ def test_deep_paths_parity():
     assert (s["extension_rays"], s["shadow_rays"]) == (rs["extension_rays"], rs["shadow_rays"])
 
 
-# (PUPIL_BVH_WIDTH, PUPIL_REFILL): BVH2, BVH4 one-ray-per-lane, BVH4 persistent with several refill thresholds
-TRAVERSALS = [("2", "16"), ("4", "0"), ("4", "1"), ("4", "16"), ("4", "64"), ("8", "1"), ("8", "24"), ("8", "64")]
+# (PUPIL_REFILL, PUPIL_NODE_MIN) of the persistent BVH4 kernel: refill thresholds from one idle lane to a
+# whole wave, node-phase exits from one lane to the whole wave
+TRAVERSALS = [("1", "8"), ("16", "8"), ("16", "1"), ("24", "64"), ("64", "8")]
 
 
 def _trace(desc, rays, any_hit=0, tmin=0.001, tmax=1e16):
@@ -228,14 +227,14 @@ def test_field_hits_random_rays_all_traversals(monkeypatch):
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.concatenate([org, d], 1).astype(np.float32)
     ref = oracle.OracleScene(desc).closest(rays)
-    for width, refill in TRAVERSALS:
-        monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+    for refill, node_min in TRAVERSALS:
         monkeypatch.setenv("PUPIL_REFILL", refill)
+        monkeypatch.setenv("PUPIL_NODE_MIN", node_min)
         out = _trace(desc, rays)
         bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
-        assert not bad.any(), f"bvh{width} refill {refill}: {bad.sum()} rays differ"
+        assert not bad.any(), f"refill {refill} node_min {node_min}: {bad.sum()} rays differ"
         occ = _trace(desc, rays, any_hit=1)
-        assert np.array_equal(occ[:, 0] > 0, ref[:, 0] > 0), f"bvh{width} refill {refill}: any-hit differs"
+        assert np.array_equal(occ[:, 0] > 0, ref[:, 0] > 0), f"refill {refill} node_min {node_min}: any-hit differs"
 
 
 @pytest.mark.parametrize("accel", ["flat", "two_level"])
@@ -296,12 +295,12 @@ def test_deep_stack_spills_match_oracle(accel, monkeypatch):
     rays = np.concatenate([org, d], 1).astype(np.float32)
     ref = oracle.OracleScene(desc).closest(rays)
     assert (ref[:, 0] > 0).mean() > 0.9
-    for width, refill in TRAVERSALS if accel == "flat" else [("4", "24")]:
-        monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+    for refill, node_min in TRAVERSALS if accel == "flat" else [("24", "8")]:
         monkeypatch.setenv("PUPIL_REFILL", refill)
+        monkeypatch.setenv("PUPIL_NODE_MIN", node_min)
         out = _trace(desc, rays)
         bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
-        assert not bad.any(), f"{accel} bvh{width} refill {refill}: {bad.sum()} rays differ"
+        assert not bad.any(), f"{accel} refill {refill} node_min {node_min}: {bad.sum()} rays differ"
 
 
 @pytest.mark.parametrize("accel", ["flat", "two_level"])
@@ -323,11 +322,11 @@ def test_tiny_scenes(ntri, accel, monkeypatch):
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.concatenate([org, d], 1).astype(np.float32)
     ref = oracle.OracleScene(desc).closest(rays)
-    for width, refill in TRAVERSALS if accel == "flat" else [("4", "24")]:
-        monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+    for refill, node_min in TRAVERSALS if accel == "flat" else [("24", "8")]:
         monkeypatch.setenv("PUPIL_REFILL", refill)
+        monkeypatch.setenv("PUPIL_NODE_MIN", node_min)
         out = _trace(desc, rays)
-        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), f"bvh{width} refill {refill}"
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), f"refill {refill} node_min {node_min}"
     gpu = render_gpu(desc, 1)
     assert np.isfinite(gpu["pt accum buffer"]).all()
 
@@ -704,12 +703,12 @@ def test_skewed_scene_stays_within_stack_capacity(accel, monkeypatch):
     rays = np.concatenate([org, d], 1).astype(np.float32)
     ref = oracle.OracleScene(desc).closest(rays)
     assert (ref[:, 0] > 0).sum() > 1000
-    for width, refill in TRAVERSALS if accel == "flat" else [("4", "24")]:
-        monkeypatch.setenv("PUPIL_BVH_WIDTH", width)
+    for refill, node_min in TRAVERSALS if accel == "flat" else [("24", "8")]:
         monkeypatch.setenv("PUPIL_REFILL", refill)
+        monkeypatch.setenv("PUPIL_NODE_MIN", node_min)
         out = _trace(desc, rays)
         bad = (out.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
-        assert not bad.any(), f"{accel} bvh{width} refill {refill}: {bad.sum()} rays differ"
+        assert not bad.any(), f"{accel} refill {refill} node_min {node_min}: {bad.sum()} rays differ"
 
 
 def _emissive_field(spheres=24, w=96, h=64, groups=2):
@@ -882,19 +881,17 @@ def test_shade_list_modes_parity(mode, monkeypatch):
         (rs["extension_rays"], rs["shadow_rays"], rs["shadow_rays_reference"])
 
 
-@pytest.mark.parametrize("family", ["bvh4", "two_level_world", "two_level_object", "bvh8", "bvh8_refill1"])
+@pytest.mark.parametrize("family", ["bvh4", "bvh4_refill1", "two_level_world", "two_level_object"])
 def test_persistent_queue_accounting(family, monkeypatch):
     """Every persistent traversal family hands out each listed ray exactly once: per
     launch, the items the XCD dequeue heads handed out = the lanes activated with them =
     the lanes retired = the list length, summed over a counter render (primary extend +
     mixed launches) and over closest-hit and any-hit ray queries.  (A round-2 experiment
-    with the spilled 6-wave BVH8 kernel once left whole 64-ray batches untraced; this is
-    the check that would catch it in any family.)"""
+    with a spilled 6-wave BVH8 kernel, since removed, once left whole 64-ray batches
+    untraced; this is the check that would catch it in any family.)"""
     from pupiloptixlab_amd.pt_pass import PTPass
 
-    if family == "bvh8" or family == "bvh8_refill1":
-        monkeypatch.setenv("PUPIL_BVH_WIDTH", "8")
-    if family == "bvh8_refill1":
+    if family == "bvh4_refill1":
         monkeypatch.setenv("PUPIL_REFILL", "1")
     if family.startswith("two_level"):
         monkeypatch.setenv("PUPIL_ACCEL", "two_level")
