@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -765,10 +766,23 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     std::vector<uint32_t> verts(n, 0), faces(n, 0), all(n);
     uint64_t wbase = 0, spheres = 0;
     for (uint32_t i = 0; i < n; i++) spheres += insts[i].kind == PUPIL_SHAPE_SPHERE ? 1u : 0u;
-    // world mode: the TLAS (at most one node per entry, <= 4^braid entries per instance) first
-    uint32_t width = 1;
-    for (uint32_t l = 0; l < acc.braid; l++) width *= 4;
-    acc.tlas_cap = acc.world ? std::max(1u, n * width) : acc.tlas_cap;
+    // world mode: the TLAS first, at most one node per entry; an instance contributes at
+    // most min(4^braid, 4 x its BLAS nodes + 1) entries (the links `braid` levels below its
+    // root), a sphere one (64-bit sum: many instances must not wrap the reserve)
+    if (acc.world) {
+        uint64_t width = 1;
+        for (uint32_t l = 0; l < acc.braid; l++) width *= 4;
+        uint64_t cap = 0;
+        for (uint32_t i = 0; i < n; i++)
+            cap += shape_of[i] == 0xFFFFFFFFu ? 1u : std::min<uint64_t>(width, 4ull * blas[shape_of[i]].num_nodes4 + 1u);
+        if (cap > kMaxNodes4) {
+            std::fprintf(stderr, "[pupil] two-level: %llu braided TLAS entries exceed the node limit, object mode\n",
+                         (unsigned long long)cap);
+            acc.world = false;
+        } else {
+            acc.tlas_cap = (uint32_t)std::max<uint64_t>(1u, cap);
+        }
+    }
     uint64_t wnodes = acc.tlas_cap;
     for (uint32_t i = 0; i < n; i++) {
         all[i] = i;
@@ -804,7 +818,11 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     acc.num_wprims = (uint32_t)wbase;
     // the traversal addresses nodes by 32-bit offsets (kMaxNodes4): instance copies beyond
     // that take the object-space structure, whose BLASes are shared
-    if (acc.world && wnodes > kMaxNodes4) acc.world = false;
+    if (acc.world && wnodes > kMaxNodes4) {
+        std::fprintf(stderr, "[pupil] two-level: %llu world BLAS copy nodes exceed the node limit, object mode\n",
+                     (unsigned long long)wnodes);
+        acc.world = false;
+    }
     if (acc.world) {  // world BLAS copies + sphere records appended to the world records
         acc.entries.assign(n, {});
         acc.inst_shape = shape_of;

@@ -391,12 +391,20 @@ uint64_t nodes4_count(const pupil_pt *pt) {
 }
 
 // DeviceScene::node_bound of the current BVH4 arrays (after every build and refit;
-// one 12-B read back, the traversal kernels take it by value)
+// one 12-B read back, the traversal kernels take it by value).  Live nodes only: in the
+// two-level layouts the TLAS reserve [tlas_nodes, tlas_cap) is never written, and
+// whatever an earlier allocation left there must not loosen the bound of every ray.
 int refresh_node_bound(pupil_pt *pt) {
     pt->sc.node_bound[0] = pt->sc.node_bound[1] = pt->sc.node_bound[2] = 0.f;
     const uint64_t n = nodes4_count(pt);
     if (!pt->sc.nodes4 || n == 0) return PUPIL_OK;
-    launch_node_bound(pt->sc.nodes4, n, pt->node_bound, pt->own_stream);
+    if (pt->two_level) {
+        const uint64_t tlas = std::min<uint64_t>(pt->tl.tlas_nodes, n), cap = std::min<uint64_t>(pt->tl.tlas_cap, n);
+        launch_node_bound(pt->sc.nodes4, tlas, pt->node_bound, pt->own_stream, true);
+        launch_node_bound(pt->sc.nodes4 + cap, n - cap, pt->node_bound, pt->own_stream, false);
+    } else {
+        launch_node_bound(pt->sc.nodes4, n, pt->node_bound, pt->own_stream, true);
+    }
     uint32_t b[3];
     HIP_TRY(hipMemcpyAsync(b, pt->node_bound, sizeof(b), hipMemcpyDeviceToHost, pt->own_stream));
     HIP_TRY(hipStreamSynchronize(pt->own_stream));

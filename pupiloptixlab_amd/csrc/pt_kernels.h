@@ -198,9 +198,9 @@ void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues
 // running mean of the batch's frames into fp.accum / fp.frame; aov_src (or null): the
 // frame's AOVs from the slot scratch (3n albedo, 3n normal, n test floats) copied to the
 // outputs; clear_flags: zero the frame's flags bytes (its ring slot is free again)
-// per axis max of |o| + 512 s over n BVH4 nodes into out[0..2] (float bits; out cleared
-// here), the bound DeviceScene::node_bound holds
-void launch_node_bound(const Bvh4Node *nodes, uint64_t n, uint32_t *out, hipStream_t s);
+// per axis max of |o| + 512 s over n BVH4 nodes into out[0..2] (float bits; clear: out is
+// zeroed first, else the max also covers what it holds), the bound DeviceScene::node_bound holds
+void launch_node_bound(const Bvh4Node *nodes, uint64_t n, uint32_t *out, hipStream_t s, bool clear = true);
 void launch_accumulate(const FrameParams &fp, const PathState &ps, const float *aov_src, bool clear_flags,
                        hipStream_t s);
 uint32_t trace_grid_blocks();

@@ -1025,8 +1025,9 @@ __global__ __launch_bounds__(256) void k_node_bound(const Bvh4Node *nodes, uint6
     }
 }
 
-void launch_node_bound(const Bvh4Node *nodes, uint64_t n, uint32_t *out, hipStream_t s) {
-    (void)hipMemsetAsync(out, 0, 3 * sizeof(uint32_t), s);
+void launch_node_bound(const Bvh4Node *nodes, uint64_t n, uint32_t *out, hipStream_t s, bool clear) {
+    if (clear) (void)hipMemsetAsync(out, 0, 3 * sizeof(uint32_t), s);
+    if (n == 0) return;
     const uint64_t blocks = std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + 255) / 256));
     hipLaunchKernelGGL(k_node_bound, dim3((uint32_t)blocks), dim3(256), 0, s, nodes, n, out);
 }

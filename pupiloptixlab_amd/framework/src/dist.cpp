@@ -7,6 +7,7 @@
 #include <cstring>
 #include <thread>
 
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include "../../../include/pupil_pt.h"
@@ -23,6 +24,18 @@ int env_int(const char *name, int def) {
 
 constexpr char kIdMagic[8] = {'P', 'U', 'P', 'I', 'L', 'I', 'D', '1'};
 
+// wall clock when this library was loaded (about when the rank process started): an id
+// file written before it, less a launcher skew allowance, belongs to an earlier launch
+const auto g_loaded = std::chrono::system_clock::now();
+constexpr int kLaunchSkewSeconds = 30;
+
+bool older_than_this_launch(const std::string &path) {
+    struct stat st;
+    if (stat(path.c_str(), &st) != 0) return false;
+    const auto loaded = std::chrono::duration_cast<std::chrono::seconds>(g_loaded.time_since_epoch()).count();
+    return (long long)st.st_mtime < (long long)loaded - kLaunchSkewSeconds;
+}
+
 // rank 0 -> the others: the 128-byte ncclUniqueId through a file, renamed into place.
 // The file carries the launch nonce (DistLaunchNonce): a file left by an earlier or
 // another launch -- a crashed run, another job on the same MASTER_PORT -- has another
@@ -36,7 +49,9 @@ bool exchange_id(const DistInfo &d, const std::string &path, ncclUniqueId &id) {
     const auto t0 = std::chrono::steady_clock::now();
     bool warned = false;
     for (;;) {
-        const int r = ReadIdFile(path, nonce, &id, sizeof(id));
+        // an id written before this launch began (a crashed run with the same launch
+        // environment) is skipped like one of another launch
+        const int r = older_than_this_launch(path) ? -1 : ReadIdFile(path, nonce, &id, sizeof(id));
         if (r > 0) return true;
         if (r < 0 && !warned) {
             Log("rank %d: ignoring %s, left by another launch (waiting for rank 0)", d.rank, path.c_str());
@@ -56,14 +71,20 @@ __global__ void k_scatter_tiles(const float4 *src, const uint32_t *map, uint32_t
 
 std::string DistLaunchNonce() noexcept {
     if (const char *n = std::getenv("PUPIL_RCCL_NONCE"); n && *n) return n;
-    // the ranks of one launch share the launcher process (torchrun's agent, mpirun, a
-    // slurm step) and its run id / restart count / port; another launch differs in one
+    // launch-wide environment only: the ranks of one launch agree on it however each rank
+    // was started (torchrun, mpirun, a slurm step, or a `timeout` wrapper per rank, whose
+    // parent processes differ), and another launch differs in its run id / restart count /
+    // job step / port.  A stale file of an earlier launch with the same environment is
+    // rejected by its age (exchange_id).
     auto env = [](const char *k) {
         const char *v = std::getenv(k);
         return std::string(v && *v ? v : "-");
     };
-    return std::to_string((long long)getppid()) + "." + env("TORCHELASTIC_RUN_ID") + "." +
-           env("TORCHELASTIC_RESTART_COUNT") + "." + env("MASTER_PORT") + "." + env("WORLD_SIZE");
+    std::string n;
+    for (const char *k : {"MASTER_ADDR", "MASTER_PORT", "WORLD_SIZE", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+                          "SLURM_JOB_ID", "SLURM_STEP_ID"})
+        n += env(k) + ".";
+    return n;
 }
 
 std::string DistIdPath() noexcept {

@@ -181,3 +181,24 @@ def test_rccl_id_file_rejects_a_stale_launch(tmp_path, monkeypatch):
     monkeypatch.setenv("TORCHELASTIC_RUN_ID", "b")
     assert lib.pupil_dist_id_path(out, 512) == 0
     assert pa.startswith(b"/tmp/pupil_rccl_29511_") and out.value != pa
+
+
+def test_rccl_id_path_agrees_across_differently_started_ranks():
+    """Ranks of one launch compute the same id file whatever process started them: here one
+    directly and one under a `timeout` wrapper (another parent process), as
+    tools/gpu_cpp_ranks.sh starts them; another run id gives another file."""
+    _built()
+    import shutil
+    import sys
+
+    code = ("import ctypes as C; lib = C.CDLL(%r); out = C.create_string_buffer(512); "
+            "lib.pupil_dist_id_path(out, 512); print(out.value.decode())" % FW)
+    env = {k: v for k, v in os.environ.items() if k != "PUPIL_RCCL_ID_FILE" and k != "PUPIL_RCCL_NONCE"}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", WORLD_SIZE="2", TORCHELASTIC_RUN_ID="r1")
+    direct = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    wrapped = subprocess.run([shutil.which("timeout"), "60", sys.executable, "-c", code], env=env,
+                             capture_output=True, text=True, check=True)
+    assert direct.stdout.strip() == wrapped.stdout.strip() != ""
+    env["TORCHELASTIC_RUN_ID"] = "r2"
+    other = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    assert other.stdout.strip() != direct.stdout.strip()

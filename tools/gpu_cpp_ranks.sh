@@ -20,5 +20,13 @@ done
 rc=0
 for p in $pids; do wait $p || rc=$?; done
 echo "ranks rc=$rc"; tail -n 3 gpurun_out/cpp_ranks/rank*.log
-[ "$rc" -eq 0 ] || exit 0
+if [ "$rc" -ne 0 ]; then
+  # RCCL refuses two ranks on one device; reaching that check means every rank found rank 0's
+  # id file (same default path and nonce) and entered ncclCommInitRank together
+  if grep -q "Duplicate GPU detected" gpurun_out/cpp_ranks/rank*.log; then
+    echo "N=$N: id exchange completed on every rank; RCCL refuses ranks sharing this box's one GPU"
+    exit 0
+  fi
+  exit $rc
+fi
 cmp gpurun_out/cpp_ranks/one.pfm gpurun_out/cpp_ranks/multi.pfm && echo "N=$N gathered image identical to 1 GPU"
