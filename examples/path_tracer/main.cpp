@@ -9,7 +9,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "pupil/denoiser.h"
@@ -24,7 +26,9 @@
 // (steady_clock around the loop); the rays are the engine's exact running total over
 // the timed OnRuns.  PUPIL_BENCH_ACCUM=<file>: the final "pt accum buffer" (rank 0,
 // raw float32 RGBA) for a bit-exact comparison with a batched render of the same
-// seeds.  Prints one JSON line.
+// seeds.  PUPIL_BENCH_MOVING=1: the interactive cadence instead -- the camera moves
+// (CameraHelper::SetCameraToWorld, a CameraChange) before every OnRun, so every frame
+// restarts accumulation and no render continues the previous one.  Prints one JSON line.
 static int Bench(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spec) {
     int warmup = 1, frames = 5, spp = 8;
     if (std::sscanf(spec, "%d,%d,%d", &warmup, &frames, &spp) != 3 || frames < 1 || spp < 1 || warmup < 0) {
@@ -32,12 +36,31 @@ static int Bench(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spe
         return 2;
     }
     Pupil::EventDispatcher<Pupil::EWorldEvent::CameraChange>();
-    for (int k = 0; k < warmup; k++) system.Run((uint32_t)spp);
+    const char *mv = std::getenv("PUPIL_BENCH_MOVING");
+    const bool moving = mv && std::atoi(mv);
+    Pupil::world::World *w = system.GetWorld();
+    float s2c[16], c2w[16];
+    w->camera->Snapshot(s2c, c2w);
+    uint32_t step = 0;
+    auto frame = [&]() {
+        if (!moving) {
+            system.Run((uint32_t)spp);
+            return;
+        }
+        for (int j = 0; j < spp; j++) {  // a camera move before every OnRun
+            float c[16];
+            std::memcpy(c, c2w, sizeof(c));
+            c[3] += 1e-4f * (float)(++step);
+            w->camera->SetCameraToWorld(c);
+            system.Run(1);
+        }
+    };
+    for (int k = 0; k < warmup; k++) frame();
     if (hipDeviceSynchronize() != hipSuccess) return 1;
     pupil_pt_counters c0{}, c1{};
     if (!pass.Stats(c0)) return 1;
     const auto t0 = std::chrono::steady_clock::now();
-    for (int k = 0; k < frames; k++) system.Run((uint32_t)spp);
+    for (int k = 0; k < frames; k++) frame();
     if (hipDeviceSynchronize() != hipSuccess) return 1;
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (!pass.Stats(c1)) return 1;
@@ -58,9 +81,79 @@ static int Bench(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spe
         std::fclose(f);
     }
     std::printf("{\"ms_per_frame\": %.4f, \"onrun_ms\": %.4f, \"mrays_per_s_rank0\": %.2f, \"rays_per_frame_rank0\": %.0f, "
-                "\"frames\": %d, \"warmup\": %d, \"spp\": %d, \"ranks\": %d, \"frames_in_flight\": %llu}\n",
+                "\"frames\": %d, \"warmup\": %d, \"spp\": %d, \"ranks\": %d, \"frames_in_flight\": %llu, "
+                "\"moving_camera\": %s, \"ring_bytes\": %llu}\n",
                 1e3 * s / frames, 1e3 * s / (frames * spp), rays / s / 1e6, rays / frames, frames, warmup, spp,
-                g ? g->Info().world : 1, (unsigned long long)c1.frames_in_flight);
+                g ? g->Info().world : 1, (unsigned long long)c1.frames_in_flight, moving ? "true" : "false",
+                (unsigned long long)c1.ring_bytes);
+    return 0;
+}
+
+// PUPIL_THREAD_TEST="k,rounds[,instance]": the reference's threading (system.cpp:93-106):
+// System::RunAsync renders on its own thread while this thread, `rounds` times, takes the
+// render lock, moves `instance` k times (each a RenderInstanceUpdate) and moves the camera
+// (a CameraChange), then lets a few frames render.  Afterwards the render thread is
+// stopped and one JSON line reports the final instance / camera matrices, the frames
+// accumulated since the last change, the acceleration refits (one per round expected:
+// PTPass refits once per OnRun however many updates it was sent) and the final
+// "pt accum buffer" (PUPIL_BENCH_ACCUM file) for a comparison with the oracle.
+static int ThreadTest(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spec) {
+    int k = 4, rounds = 3, inst = 0;
+    if (std::sscanf(spec, "%d,%d,%d", &k, &rounds, &inst) < 2 || k < 1 || rounds < 1) return 2;
+    Pupil::world::World *w = system.GetWorld();
+    if (inst < 0 || (uint32_t)inst >= w->Desc().num_instances) return 2;
+    float base[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1};
+    std::memcpy(base, w->Desc().instances[inst].to_world, 12 * sizeof(float));
+    float s2c[16], cam[16];
+    w->camera->Snapshot(s2c, cam);
+    int updates = 0;
+    float m[16], c[16];
+    system.RunAsync();
+    auto wait_frames = [&](uint64_t n) {
+        const uint64_t f0 = system.FramesRendered();
+        while (system.FramesRendered() < f0 + n) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    };
+    wait_frames(3);
+    for (int r = 1; r <= rounds; r++) {
+        {
+            auto lock = system.RenderLock();
+            for (int j = 1; j <= k; j++) {  // absolute moves: the last one of the round stays
+                std::memcpy(m, base, sizeof(m));
+                m[3] += 0.01f * (float)((r - 1) * k + j);
+                m[7] += 0.005f * (float)j;
+                w->SetInstanceTransform((uint32_t)inst, m);
+                updates++;
+            }
+            std::memcpy(c, cam, sizeof(c));
+            c[3] += 0.002f * (float)r;  // camera position x
+            w->camera->SetCameraToWorld(c);
+        }
+        wait_frames(2 + (uint64_t)r);
+    }
+    system.Stop();
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    pupil_pt_counters cnt{};
+    if (!pass.Stats(cnt)) return 1;
+    if (const char *path = std::getenv("PUPIL_BENCH_ACCUM")) {
+        auto *buf = Pupil::BufferManager::instance()->GetBuffer("pt accum buffer");
+        const size_t n = buf ? (size_t)buf->desc.width * buf->desc.height * 4 : 0;
+        std::vector<float> host(n);
+        FILE *f = nullptr;
+        if (!buf || hipMemcpy(host.data(), buf->cuda_ptr, n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess ||
+            !(f = std::fopen(path, "wb")) || std::fwrite(host.data(), sizeof(float), n, f) != n) {
+            if (f) std::fclose(f);
+            return 1;
+        }
+        std::fclose(f);
+    }
+    std::printf("{\"updates\": %d, \"rounds\": %d, \"accel_refits\": %llu, \"frames_rendered\": %llu, "
+                "\"frames_accumulated\": %u, \"instance\": %d, \"to_world\": [",
+                updates, rounds, (unsigned long long)cnt.accel_refits, (unsigned long long)system.FramesRendered(),
+                pass.SampleCount(), inst);
+    for (int i = 0; i < 16; i++) std::printf("%s%.9g", i ? ", " : "", m[i]);
+    std::printf("], \"camera_to_world\": [");
+    for (int i = 0; i < 16; i++) std::printf("%s%.9g", i ? ", " : "", c[i]);
+    std::printf("]}\n");
     return 0;
 }
 
@@ -90,6 +183,8 @@ int main(int argc, char **argv) {
             rc = 1;
         } else if (const char *bench = std::getenv("PUPIL_BENCH")) {
             rc = Bench(*system, *pt_pass, bench);
+        } else if (const char *tt = std::getenv("PUPIL_THREAD_TEST")) {
+            rc = ThreadTest(*system, *pt_pass, tt);
         } else {
             system->Run((uint32_t)frames);
             pt_pass->Inspector();

@@ -279,6 +279,18 @@ typedef struct pupil_pt_counters {
     uint64_t queue_activated;
     uint64_t queue_retired;
     uint64_t queue_listed;
+    /* ABI 4.  HBM held by the pipelined-frame ring (path state, queues, AOV scratch) and
+     * the budget it may grow to (PUPIL_PIPE_GB, default a quarter of the device memory
+     * free at pupil_pt_create) */
+    uint64_t ring_bytes;
+    uint64_t ring_budget_bytes;
+    /* acceleration structure refits / rebuilds done for instance updates since creation:
+     * one per pupil_pt_update_instances call, however many instances it moves */
+    uint64_t accel_refits;
+    /* DeviceScene::node_bound, the per-axis max of |o| + 512 s over the live BVH4 nodes
+     * (the slab test's rounding bound is taken per ray from it) */
+    float node_bound[3];
+    uint32_t pad_counters;
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;
@@ -291,7 +303,15 @@ int pupil_pt_set_camera(pupil_pt *pt, const float sample_to_camera[16], const fl
 /* instance = index into pupil_scene_desc.instances; to_world / to_object row-major 3x4.
  * Must not overlap a render in flight (the reference serialises both under its render mutex). */
 int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_world[12], const float to_object[12]);
-/* replaces the area-emitter table, selection CDF and env emitter (after an emissive instance moved) */
+/* n instances at once: ids[k] gets to_world[12k..12k+11] / to_object[12k..]; ONE refit of
+ * the acceleration structure covers them all (the reference refits its IAS once per OnRun,
+ * however many RenderInstanceUpdate events marked it dirty: pt_pass.cpp:46,216-218).
+ * Ordered after every render enqueued so far (stream events, no device-wide sync); returns
+ * when the structure is updated.  pupil_pt_update_instance = n = 1. */
+int pupil_pt_update_instances(pupil_pt *pt, uint32_t n, const uint32_t *ids, const float *to_world,
+                              const float *to_object);
+/* replaces the area-emitter table, selection CDF and env emitter (after an emissive instance moved);
+ * rewritten in place on the engine's stream when their shapes are unchanged */
 int pupil_pt_update_emitters(pupil_pt *pt, const pupil_scene_desc *scene);
 /* Asynchronous on hip_stream (a hipStream_t; NULL = the default null stream): the
  * output buffers are complete once work later enqueued on that stream runs. */
@@ -318,6 +338,10 @@ int pupil_debug_math(int device, uint32_t n, const float *x, const float *y2, fl
 /* the device's emitter pick (EmitterGroup::SelectOneEmiiter, render/emitter.h:110-135)
  * for n random numbers p: out[i] = area emitter index, -1 = env, -2 = none */
 int pupil_debug_select_emitter(pupil_pt *pt, uint32_t n, const float *p, int32_t *out);
+/* two-level structure: fills the never-written TLAS reserve [tlas_nodes, tlas_cap) of the
+ * node array with nodes whose every float is `value`, then recomputes node_bound (test of
+ * the bound's live-node ranges); PUPIL_ERR_UNSUPPORTED for the flattened BVH */
+int pupil_debug_fill_tlas_reserve(pupil_pt *pt, float value);
 
 /* ---- image output (util::BitmapTexture::Save, framework/util/texture.cpp:12-85,152-160) ----
  * rgba: width*height float4, row 0 = image bottom (the "final result" order).

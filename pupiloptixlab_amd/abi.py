@@ -92,10 +92,13 @@ class Counters(C.Structure):
                 ("rays_traced_total", C.c_uint64), ("frames_in_flight", C.c_uint64),
                 ("pipeline_slots", C.c_uint64), ("tlas_sah_splits", C.c_uint64),
                 ("queue_handed", C.c_uint64), ("queue_activated", C.c_uint64), ("queue_retired", C.c_uint64),
-                ("queue_listed", C.c_uint64)]
+                ("queue_listed", C.c_uint64), ("ring_bytes", C.c_uint64), ("ring_budget_bytes", C.c_uint64),
+                ("accel_refits", C.c_uint64), ("node_bound", C.c_float * 3), ("pad_counters", C.c_uint32)]
 
     def as_dict(self):
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        d = {name: getattr(self, name) for name, _ in self._fields_ if name != "pad_counters"}
+        d["node_bound"] = [float(x) for x in self.node_bound]
+        return d
 
 
 DENOISE_USE_ALBEDO, DENOISE_USE_NORMAL, DENOISE_APPLY_TO_AOV = 1, 2, 4
@@ -114,7 +117,9 @@ SIGNATURES = {
     "pupil_pt_create": (C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "pupil_pt_set_camera": (C.c_int, [C.c_void_p, f32p, f32p]),
     "pupil_pt_update_instance": (C.c_int, [C.c_void_p, C.c_uint32, f32p, f32p]),
+    "pupil_pt_update_instances": (C.c_int, [C.c_void_p, C.c_uint32, u32p, f32p, f32p]),
     "pupil_pt_update_emitters": (C.c_int, [C.c_void_p, C.POINTER(SceneDesc)]),
+    "pupil_debug_fill_tlas_reserve": (C.c_int, [C.c_void_p, C.c_float]),
     "pupil_pt_render": (C.c_int, [C.c_void_p, C.POINTER(Frame), C.POINTER(Launch), C.c_void_p]),
     "pupil_pt_stats": (C.c_int, [C.c_void_p, C.POINTER(Counters)]),
     "pupil_pt_local_pixels": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,

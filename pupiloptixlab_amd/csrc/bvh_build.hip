@@ -1282,12 +1282,13 @@ namespace {
 
 // Records of the moved instance (b.w = instance) get its new world vertices, written
 // exactly as k_prim_setup writes them (global id in a.w: sphere bit + id).
-__global__ void k_refit_records(BvhBuildInput in, uint32_t n, float4 *recs, uint32_t moved) {
+__global__ void k_refit_records(BvhBuildInput in, uint32_t n, float4 *recs, const uint8_t *moved) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
-    if (__float_as_uint(recs[3 * r + 1].w) != moved) return;
+    const uint32_t id = __float_as_uint(recs[3 * r + 1].w);
+    if (!moved[id]) return;
     const uint32_t gid = __float_as_uint(recs[3 * r].w) & ~kPrimSphereBit;
-    const DevInstance &inst = in.instances[moved];
+    const DevInstance &inst = in.instances[id];
     if (inst.kind == PUPIL_SHAPE_SPHERE) {
         const float *m = inst.to_world;
         const vec3 c = v3(m[3], m[7], m[11]);
@@ -1367,15 +1368,15 @@ __global__ void k_refit_level(Bvh4Node *nodes, uint32_t lo, uint32_t hi, const f
 
 }  // namespace
 
-int refit_bvh4(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t moved, hipStream_t s, double *ms) {
+int refit_bvh4(const BvhBuildInput &in, BvhBuildOutput &out, const uint8_t *moved, float *nbox, hipStream_t s,
+               double *ms) {
     if (out.level_start.size() < 2 || !out.nodes4 || out.num_nodes4 == 0) return -1;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, s);
-    float *nbox = nullptr;
-    hipError_t err = dmalloc(&nbox, 6 * (size_t)out.num_nodes4);
-    if (!err) {
+    hipError_t err = hipSuccess;
+    {
         const uint32_t n = in.num_prims;
         hipLaunchKernelGGL(k_refit_records, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, in, n, out.prims, moved);
         for (size_t L = out.level_start.size() - 1; L-- > 0;) {
@@ -1392,7 +1393,6 @@ int refit_bvh4(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t moved, hip
     if (ms) *ms = t;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    if (nbox) (void)hipFree(nbox);
     return err == hipSuccess ? 0 : -2;
 }
 

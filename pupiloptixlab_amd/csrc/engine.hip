@@ -24,6 +24,10 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// most event pairs pending at once: a PUPIL_STATS_TRACE_TIMING sequence that is never
+// read folds its pairs into sums at this count, a deep timed render stops recording
+constexpr uint32_t kMaxPairs = 4096;
+
 int fail(int code, const std::string &msg) {
     g_last_error = msg;
     return code;
@@ -117,9 +121,14 @@ struct pupil_pt {
     size_t pipe_np = 0;               // paths per slot
     uint32_t pipe_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // w, h, tile size, rank, world, spp, depth, local pixels
     uint32_t pipe_run = 0;            // consecutive renders that continued the previous one
+    uint32_t pipe_next_seed = 0;      // random_seed of the render that would continue the last one
     uint32_t pipe_gen = 0;            // iterations so far (flags tags)
     uint32_t pipe_limit = 0;          // PUPIL_PIPE: most slots (0 = max_depth)
-    double pipe_budget = 160e9;       // PUPIL_PIPE_GB: most HBM bytes for the ring's path state (of 288 GB)
+    // PUPIL_PIPE_GB: most HBM bytes for the ring's path state; default a quarter of the
+    // device memory free when the engine was created (config 4 needs 9.5 GB, config 5 19 GB
+    // of a 288 GB MI355X), so a drop-in pass leaves the rest of a shared device to others
+    double pipe_budget = 0.0;
+    uint64_t ring_bytes = 0;          // path state + queues + AOV scratch allocated now
     // PUPIL_PIPE_PATHS: a ring needs no more slots than it takes to put this many paths in
     // flight.  Frames ahead pay off by filling the launch tails of small launches; past
     // ~64 M paths per launch the tail is amortised and a larger ring only spreads the
@@ -144,9 +153,11 @@ struct pupil_pt {
     uint32_t pm_count = 0;
     // stats
     unsigned long long *trace_counters = nullptr;  // [0] nodes [1] prims
-    uint32_t *ray_log = nullptr;                   // per iteration of the last render: next, shadow
-    uint32_t ray_log_cap = 0;                      // iterations it holds
-    unsigned long long *ray_cum = nullptr;         // device running totals: next, shadow rays
+    // device running totals of the extension and shadow rays listed by the flags partitions
+    // ([0..1]); the first partition of a render copies them to [2..3] before adding, so the
+    // render's own counts are [0..1] - [2..3] without a per-render clear (snap_taken)
+    unsigned long long *ray_cum = nullptr;
+    bool snap_taken = false;
     uint32_t *node_bound = nullptr;                // launch_node_bound's result (3 floats as bits)
     uint64_t primary_cum = 0;                      // host running total of camera rays
     uint32_t last_paths = 0, last_iters = 0;
@@ -154,9 +165,16 @@ struct pupil_pt {
     bool last_stats = false;
     std::vector<hipEvent_t> trace_events;  // pairs
     std::vector<uint8_t> pair_kind;        // per pair: 0 extend, 1 shadow, 2 shade
-    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    // ev_begin / ev_end bracket renders that collect counters or stage times only (each event
+    // leaves a few us of stream gap); ev_sync orders another stream after the last render
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_sync = nullptr;
+    bool last_timed = false;  // the last render recorded ev_begin / ev_end
     uint32_t trace_pairs = 0;
     bool pairs_keep = false;  // the pairs of PUPIL_STATS_TRACE_TIMING renders accumulate until read
+    // pairs of a PUPIL_STATS_TRACE_TIMING sequence folded into sums once kMaxPairs are pending
+    double kept_ms[3] = {0.0, 0.0, 0.0};
+    uint64_t kept_n[3] = {0, 0, 0};
+    uint64_t refits = 0;  // acceleration structure refits / rebuilds after instance updates
     // PUPIL_TRACE_TAIL: per-wave start / drained / exit times of each traversal launch of a stats render
     unsigned long long *tail_buf = nullptr;
     uint32_t tail_waves = 0, tail_launches = 0;
@@ -169,6 +187,15 @@ struct pupil_pt {
     DevEmitter *d_areas = nullptr, *d_env = nullptr;
     float *d_cdf = nullptr;
     uint32_t *d_guide = nullptr;
+    pupil_emitter env_src{};  // the env emitter the tables were built from (same_env)
+    bool env_src_valid = false;
+    std::vector<DevEmitter> h_emit_areas;  // host sources of in-place emitter updates
+    std::vector<float> h_emit_cdf;
+    std::vector<uint32_t> h_emit_guide;
+    // flattened-BVH refits: per-instance moved flags and the node-box scratch
+    uint8_t *d_moved = nullptr;
+    std::vector<uint8_t> h_moved;
+    float *refit_box = nullptr;
 
     template <typename T>
     hipError_t alloc(T **p, size_t count) {
@@ -192,6 +219,7 @@ struct pupil_pt {
         (void)hipFree(p);
     }
     void release_state() {
+        ring_bytes = 0;
         void *bufs[] = {ps.ray_o, ps.ray_d, ps.hit,  ps.thr,  ps.rad,    ps.misc,
                         ps.sh_d, ps.sh_c, ps.mbin, ps.sflags, q.bins, q.nxsh, q.hist};
         for (void *b : bufs)
@@ -206,7 +234,6 @@ struct pupil_pt {
         (void)hipSetDevice(device);
         release_state();
         if (aov_scratch) (void)hipFree(aov_scratch);
-        if (ray_log) (void)hipFree(ray_log);
         for (void *p : allocs) (void)hipFree(p);
         free_lbvh(bvh);
         free_two_level(tl);
@@ -214,6 +241,7 @@ struct pupil_pt {
         for (auto e : trace_events) (void)hipEventDestroy(e);
         if (ev_begin) (void)hipEventDestroy(ev_begin);
         if (ev_end) (void)hipEventDestroy(ev_end);
+        if (ev_sync) (void)hipEventDestroy(ev_sync);
         if (own_stream) (void)hipStreamDestroy(own_stream);
     }
 };
@@ -305,11 +333,14 @@ int convert_emitter(pupil_pt *pt, const pupil_emitter &e, DevEmitter &d) {
     return PUPIL_OK;
 }
 
-// EmitterGroup (render/emitter.h:110-135): area emitters, their sequential
-// selection CDF and the env emitter; replaces the previous tables (updates).
-int upload_emitters(pupil_pt *pt, const pupil_scene_desc *scene) {
-    std::vector<DevEmitter> areas(scene->num_area_emitters);
-    std::vector<float> cdf(scene->num_area_emitters);
+// EmitterGroup (render/emitter.h:110-135): the area emitters, their sequential selection
+// CDF and its guide table (2^bits >= emitter count buckets, at most 2^20, guide[k] = first
+// i with cdf[i] >= k / 2^bits; empty for PUPIL_EMITTER_SELECT=binary, the plain binary
+// search A/B, or fewer than two emitters).  Bitmap radiance textures are uploaded here.
+int emitter_tables(pupil_pt *pt, const pupil_scene_desc *scene, std::vector<DevEmitter> &areas, std::vector<float> &cdf,
+                   std::vector<uint32_t> &guide, uint32_t &bits) {
+    areas.assign(scene->num_area_emitters, DevEmitter{});
+    cdf.assign(scene->num_area_emitters, 0.f);
     float sum_p = 0.f;
     for (uint32_t e = 0; e < scene->num_area_emitters; e++) {
         int rc = convert_emitter(pt, scene->area_emitters[e], areas[e]);
@@ -317,29 +348,47 @@ int upload_emitters(pupil_pt *pt, const pupil_scene_desc *scene) {
         cdf[e] = sum_p + areas[e].select_probability;
         sum_p = cdf[e];
     }
+    bits = 0;
+    while ((1u << bits) < scene->num_area_emitters && bits < 20) bits++;
+    const char *sel = std::getenv("PUPIL_EMITTER_SELECT");
+    guide.clear();
+    if (scene->num_area_emitters > 1 && !(sel && std::strcmp(sel, "binary") == 0)) {
+        const uint32_t m = 1u << bits;
+        guide.resize(m + 1);
+        uint32_t i = 0;
+        for (uint32_t k = 0; k <= m; k++) {
+            const float t = (float)k / (float)m;
+            while (i < cdf.size() && cdf[i] < t) i++;
+            guide[k] = i;
+        }
+    }
+    return PUPIL_OK;
+}
+
+// the scene's env emitter is the one the engine holds (an update may then keep its tables)
+bool same_env(const pupil_pt *pt, const pupil_scene_desc *scene) {
+    const bool has = scene->env && scene->env->type != PUPIL_EMITTER_NONE;
+    if (has != pt->env_src_valid) return false;
+    return !has || std::memcmp(&pt->env_src, scene->env, sizeof(pupil_emitter)) == 0;
+}
+
+// replaces the previous tables (creation, and updates that change their shapes)
+int upload_emitters(pupil_pt *pt, const pupil_scene_desc *scene) {
+    std::vector<DevEmitter> areas;
+    std::vector<float> cdf;
+    std::vector<uint32_t> g;
+    uint32_t bits = 0;
+    if (const int rc = emitter_tables(pt, scene, areas, cdf, g, bits)) return rc;
     DevEmitter *d_areas = nullptr, *d_env = nullptr;
     float *d_cdf = nullptr;
     uint32_t *d_guide = nullptr;
     if (pt->upload(&d_areas, areas.data(), areas.size()) || pt->upload(&d_cdf, cdf.data(), cdf.size()))
         return fail(PUPIL_ERR_OOM, "emitter upload failed");
-    // guide table: 2^bits >= emitter count buckets (at most 2^20), guide[k] = first i
-    // with cdf[i] >= k / 2^bits (PUPIL_EMITTER_SELECT=binary: plain binary search, A/B)
-    uint32_t bits = 0;
-    while ((1u << bits) < scene->num_area_emitters && bits < 20) bits++;
-    const char *sel = std::getenv("PUPIL_EMITTER_SELECT");
-    const bool guide = scene->num_area_emitters > 1 && !(sel && std::strcmp(sel, "binary") == 0);
-    if (guide) {
-        const uint32_t m = 1u << bits;
-        std::vector<uint32_t> g(m + 1);
-        uint32_t i = 0;
-        for (uint32_t k = 0; k <= m; k++) {
-            const float t = (float)k / (float)m;
-            while (i < cdf.size() && cdf[i] < t) i++;
-            g[k] = i;
-        }
-        if (pt->upload(&d_guide, g.data(), g.size())) return fail(PUPIL_ERR_OOM, "emitter guide upload failed");
-    }
+    if (!g.empty() && pt->upload(&d_guide, g.data(), g.size())) return fail(PUPIL_ERR_OOM, "emitter guide upload failed");
+    pt->env_src_valid = false;
     if (scene->env && scene->env->type != PUPIL_EMITTER_NONE) {
+        pt->env_src = *scene->env;
+        pt->env_src_valid = true;
         DevEmitter env;
         int rc = convert_emitter(pt, *scene->env, env);
         if (rc) return rc;
@@ -382,10 +431,19 @@ int ensure_state(pupil_pt *pt, size_t paths) {
     HIP_TRY(hipMalloc((void **)&pt->q.hist, sizeof(uint32_t) * partition_hist_entries((uint32_t)n)));
     pt->q.capacity = (uint32_t)n;
     pt->cap = n;
+    pt->ring_bytes = n * (8 * 16 + 2 + 4 + 8) + sizeof(uint32_t) * (size_t)partition_hist_entries((uint32_t)n);
     return PUPIL_OK;
 }
 
 // BVH4 node array the traversal walks (its size bounds the 32-bit node offsets, kMaxNodes4)
+// the engine's own stream waits for everything enqueued so far on the stream of the last
+// render (which itself waited for the renders before it on other streams)
+hipError_t order_after_renders(pupil_pt *pt) {
+    if (!pt->rendered || pt->last_stream == pt->own_stream) return hipSuccess;
+    hipError_t e = hipEventRecord(pt->ev_sync, pt->last_stream);
+    return e == hipSuccess ? hipStreamWaitEvent(pt->own_stream, pt->ev_sync, 0) : e;
+}
+
 uint64_t nodes4_count(const pupil_pt *pt) {
     return pt->two_level ? (pt->tl.world ? pt->tl.num_wnodes : pt->tl.num_nodes4) : pt->bvh.num_nodes4;
 }
@@ -449,8 +507,9 @@ struct RenderCtx {
     const TraceStats *tsp() const { return stats ? &ts_dev : nullptr; }
     // stage events only on request: each hipEventRecord between two kernels costs
     // ~6 us of stream gap (9 per 1-spp render at D = 4)
+    uint32_t pair_cap = 0;  // events created for this render
     void ev0(uint8_t kind) {
-        open = timing && !(trace_only && kind == 2);
+        open = timing && !(trace_only && kind == 2) && pair < pair_cap;
         if (!open) return;
         pt->pair_kind[pair] = kind;
         (void)hipEventRecord(pt->trace_events[2 * pair], s);
@@ -513,8 +572,11 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         while (K > 1 && (uint64_t)K * np >= (1ull << 31)) K--;
     }
     const uint32_t key[8] = {cx.key[0], cx.key[1], cx.key[2], cx.key[3], cx.key[4], fp.spp, D, fp.num_local};
-    bool reset = !(pt->pipe_valid && !pt->pipe.empty() && K == pt->pipe_slots && np == pt->pipe_np &&
-                   std::memcmp(key, pt->pipe_key, sizeof(key)) == 0 && pt->pipe.front().seed == launch->random_seed);
+    // this render continues the last one (OnRun cadence: the next seed, nothing changed);
+    // frames in flight, if any, are then exactly the ones it and its successors need
+    bool reset = !(pt->pipe_valid && K == pt->pipe_slots && np == pt->pipe_np &&
+                   std::memcmp(key, pt->pipe_key, sizeof(key)) == 0 && pt->pipe_next_seed == launch->random_seed &&
+                   (pt->pipe.empty() || pt->pipe.front().seed == launch->random_seed));
     if ((size_t)K * np > pt->cap) {  // growing the ring loses its contents
         reset = true;
         int rc = ensure_state(pt, (size_t)K * np);
@@ -554,11 +616,19 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
     const uint32_t L = pt->pipe.empty() ? D : D - pt->pipe.front().phases;
     auto scratch = [&](uint32_t slot) { return pt->aov_scratch + (size_t)slot * 7 * nl; };
     uint64_t started = 0;
+    // frames ahead are started only once a continuation is likely: the caller said so
+    // (PUPIL_HINT_CONTINUE), or this render already continued the previous one.  A render
+    // after a change (a camera moving every OnRun) then traces nothing it may discard.
+    const bool speculate = (launch->hints & PUPIL_HINT_CONTINUE) || pt->pipe_run >= 1 || pt->ahead_mode == 2;
+    // depths above 64: every 16 iterations the host reads the list lengths back and stops
+    // once no path is left (all of them missed, were absorbed or were terminated by RR)
+    const bool deep_exit = D > 64 && K == 1;
+    pt->snap_taken = false;
     for (uint32_t it = 0; it < L; it++) {
         const bool had = !pt->pipe.empty();
         // start a frame: this render's own on an empty pipeline, else the next one ahead
         // in the last run + 1 iterations while a slot is free
-        const bool inject = !had || (pt->pipe.size() < K && it + pt->pipe_run + 1 >= L);
+        const bool inject = !had || (speculate && pt->pipe.size() < K && it + pt->pipe_run + 1 >= L);
         pupil_pt::PipeFrame nf{0u, launch->random_seed, 0u, false};
         if (inject) {
             if (had) {
@@ -576,7 +646,15 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
             // increasing path id: next (bit 0) and shadow (bit 1) lists -> q.nxsh
             const uint32_t tag = pt->pipe_gen % 63u + 1u;
             launch_partition(ring.sflags, nring, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
-                             q.counts + kStartNext, nullptr, pt->ray_log + 2 * it, s, pt->ray_cum);
+                             q.counts + kStartNext, nullptr, nullptr, s, pt->ray_cum,
+                             pt->snap_taken ? nullptr : pt->ray_cum + 2);
+            pt->snap_taken = true;
+            if (deep_exit && it % 16 == 0) {
+                uint32_t c[2] = {1, 1};
+                HIP_TRY(hipMemcpyAsync(c, q.counts + kCntNext, sizeof(c), hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                if (c[0] == 0 && c[1] == 0) break;  // nothing left to trace or shade: the frame is complete
+            }
             cx.ev0(1);
             cx.tail_slot();
             if (inject)  // + the new frame's camera rays, dequeued first in every chunk (pixel-major)
@@ -622,6 +700,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
     const pupil_pt::PipeFrame f = pt->pipe.front();
     pt->pipe.erase(pt->pipe.begin());
     launch_accumulate(fp, cx.view(f.slot, np), f.aov_scratch ? scratch(f.slot) : nullptr, K > 1, s);
+    pt->pipe_next_seed = launch->random_seed + fp.spp;
     pt->last_iters = L;
     pt->last_primary = started * np;
     pt->primary_cum += started * np;
@@ -633,7 +712,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
 extern "C" {
 
 const char *pupil_last_error(void) { return g_last_error.c_str(); }
-int pupil_abi_version(void) { return 3; }
+int pupil_abi_version(void) { return 4; }
 
 int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank, uint32_t tile_world,
                           uint32_t *out_pixels, uint32_t *inout_count) {
@@ -869,13 +948,14 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     // traversal overflow stacks, counters, events
     pt->ovf_threads = trace_grid_blocks() * (uint32_t)kTraceBlock;
     if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 32) ||
-        pt->alloc(&pt->ray_cum, 2) || pt->alloc(&pt->node_bound, 3) || pt->alloc(&pt->q.counts, kCountSlots) ||
+        pt->alloc(&pt->ray_cum, 4) || pt->alloc(&pt->node_bound, 3) || pt->alloc(&pt->q.counts, kCountSlots) ||
         pt->alloc(&pt->q.work, kWorkSlots))
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
     if (hipMemset(pt->q.work, 0, kWorkSlots * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(pt->ray_cum, 0, 2 * sizeof(unsigned long long)) != hipSuccess)
+        hipMemset(pt->ray_cum, 0, 4 * sizeof(unsigned long long)) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "workspace clear failed"));
-    if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess)
+    if (hipEventCreate(&pt->ev_begin) != hipSuccess || hipEventCreate(&pt->ev_end) != hipSuccess ||
+        hipEventCreateWithFlags(&pt->ev_sync, hipEventDisableTiming) != hipSuccess)
         return cleanup(fail(PUPIL_ERR_HIP, "event creation failed"));
     if (refresh_node_bound(pt) != PUPIL_OK) return cleanup(PUPIL_ERR_HIP);
     pt->totals.bvh_nodes = pt->two_level ? two_level_nodes(pt->tl) : pt->bvh.num_nodes4;
@@ -897,27 +977,44 @@ int pupil_pt_set_camera(pupil_pt *pt, const float sample_to_camera[16], const fl
     return PUPIL_OK;
 }
 
-// RenderInstanceUpdate (ias_manager.cpp:116-151): new instance transform, then
-// the acceleration structure is rebuilt over the updated world-space primitives
-// (LBVH build, ~8 ms per 1M primitives); the render after it is identical to a
-// render of a freshly created engine.  Emitters follow with pupil_pt_update_emitters.
-int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_world[12], const float to_object[12]) {
-    if (!pt || !to_world || !to_object) return fail(PUPIL_ERR_INVALID, "null argument");
-    if (instance >= pt->h_insts.size()) return fail(PUPIL_ERR_INVALID, "instance index out of range");
+// RenderInstanceUpdate (ias_manager.cpp:116-151) for a set of instances: their new
+// transforms, then ONE refit of the acceleration structure over all of them (the
+// reference marks its IAS dirty per event and refits once in the next OnRun through
+// GetIASHandle(2, true), pt_pass.cpp:46, ias_manager.cpp:199-211).  Flattened BVH: the
+// moved instances' records get their new world vertices and every BVH4 node is refitted
+// bottom up; two-level: their world records / BLAS copies and the TLAS boxes are
+// refitted.  The render after it equals a render of a freshly created engine.  Ordered
+// on the engine's stream after every render enqueued so far (no device-wide sync: other
+// streams of the process keep running); returns once the structure is updated.
+// Emitters follow with pupil_pt_update_emitters.
+int pupil_pt_update_instances(pupil_pt *pt, uint32_t n, const uint32_t *ids, const float *to_world,
+                              const float *to_object) {
+    if (!pt || (n && (!ids || !to_world || !to_object))) return fail(PUPIL_ERR_INVALID, "null argument");
+    for (uint32_t k = 0; k < n; k++)
+        if (ids[k] >= pt->h_insts.size()) return fail(PUPIL_ERR_INVALID, "instance index out of range");
+    if (n == 0) return PUPIL_OK;
     HIP_TRY(hipSetDevice(pt->device));
-    HIP_TRY(hipDeviceSynchronize());  // no render may still read the old tables
-    pt->pipe_valid = false;           // frames in flight were traced against the old geometry
-    DevInstance &d = pt->h_insts[instance];
-    std::memcpy(d.to_world, to_world, sizeof(d.to_world));
-    std::memcpy(d.to_object, to_object, sizeof(d.to_object));
-    if (pt->two_level) refresh_instance_margins(d);  // they depend on the transform
-    HIP_TRY(hipMemcpy(pt->d_insts + instance, &d, sizeof(DevInstance), hipMemcpyHostToDevice));
-    if (pt->two_level) {  // new world box for the instance, TLAS rebuilt over all instance boxes
+    HIP_TRY(order_after_renders(pt));  // no render may still read the old tables
+    pt->pipe_valid = false;             // frames in flight were traced against the old geometry
+    std::vector<uint32_t> changed;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t id = ids[k];
+        DevInstance &d = pt->h_insts[id];
+        std::memcpy(d.to_world, to_world + 12 * (size_t)k, sizeof(d.to_world));
+        std::memcpy(d.to_object, to_object + 12 * (size_t)k, sizeof(d.to_object));
+        if (pt->two_level) refresh_instance_margins(d);  // they depend on the transform
+        if (std::find(changed.begin(), changed.end(), id) == changed.end()) changed.push_back(id);
+    }
+    for (uint32_t id : changed)  // h_insts outlives the copies (the stream is synchronised below)
+        HIP_TRY(hipMemcpyAsync(pt->d_insts + id, &pt->h_insts[id], sizeof(DevInstance), hipMemcpyHostToDevice,
+                               pt->own_stream));
+    pt->refits++;
+    if (pt->two_level) {
         const auto t0 = std::chrono::steady_clock::now();
         // world mode refits the TLAS like the reference's IAS update (PUPIL_TL_UPDATE=rebuild: full build)
         const char *um = std::getenv("PUPIL_TL_UPDATE");
         const bool refit = !(um && std::strcmp(um, "rebuild") == 0);
-        const int trc = rebuild_tlas(pt->tl, pt->h_insts, pt->d_insts, {instance}, pt->own_stream, refit);
+        const int trc = rebuild_tlas(pt->tl, pt->h_insts, pt->d_insts, changed, pt->own_stream, refit);
         if (trc == -3) return fail(PUPIL_ERR_UNSUPPORTED, "TLAS + BLAS deeper than the traversal stacks hold");
         if (trc != 0) return fail(PUPIL_ERR_HIP, "TLAS rebuild failed");
         pt->sc.root_link4 = pt->tl.root_link4;
@@ -931,8 +1028,13 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     // refit in place (PUPIL_FLAT_UPDATE=rebuild: full rebuild)
     const char *fu = std::getenv("PUPIL_FLAT_UPDATE");
     if (!(fu && std::strcmp(fu, "rebuild") == 0)) {
+        if (!pt->d_moved) HIP_TRY(pt->alloc(&pt->d_moved, pt->h_insts.size()));
+        if (!pt->refit_box) HIP_TRY(pt->alloc(&pt->refit_box, 6 * (size_t)std::max(1u, pt->bvh.num_nodes4)));
+        pt->h_moved.assign(pt->h_insts.size(), 0);
+        for (uint32_t id : changed) pt->h_moved[id] = 1;
+        HIP_TRY(hipMemcpyAsync(pt->d_moved, pt->h_moved.data(), pt->h_moved.size(), hipMemcpyHostToDevice, pt->own_stream));
         double rms = 0.0;
-        if (refit_bvh4(bin, pt->bvh, instance, pt->own_stream, &rms) == 0) {
+        if (refit_bvh4(bin, pt->bvh, pt->d_moved, pt->refit_box, pt->own_stream, &rms) == 0) {
             pt->totals.build_ms = rms;
             return refresh_node_bound(pt);
         }
@@ -947,6 +1049,10 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     }
     free_lbvh(pt->bvh);
     pt->bvh = nb;
+    if (pt->refit_box) {  // sized for the old tree
+        pt->release(pt->refit_box);
+        pt->refit_box = nullptr;
+    }
     pt->sc.prims = nb.prims;
     pt->sc.attrs = nb.attrs;
     pt->sc.nodes4 = nb.nodes4;
@@ -957,14 +1063,48 @@ int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_wor
     return refresh_node_bound(pt);
 }
 
+int pupil_pt_update_instance(pupil_pt *pt, uint32_t instance, const float to_world[12], const float to_object[12]) {
+    if (!pt || !to_world || !to_object) return fail(PUPIL_ERR_INVALID, "null argument");
+    return pupil_pt_update_instances(pt, 1, &instance, to_world, to_object);
+}
+
 // EmitterHelper reset after a transform change (world/world.cpp:45-54): the area
-// emitter table, selection CDF and env emitter are replaced by the scene's.
+// emitter table, selection CDF and env emitter are replaced by the scene's.  When the
+// tables keep their shapes (same emitter count, no bitmap radiance to upload, the same
+// env) they are rewritten in place on the engine's stream after the renders enqueued so
+// far; otherwise new tables are uploaded and the old ones freed.
 int pupil_pt_update_emitters(pupil_pt *pt, const pupil_scene_desc *scene) {
     if (!pt || !scene) return fail(PUPIL_ERR_INVALID, "null argument");
     if (scene->num_area_emitters && !scene->area_emitters) return fail(PUPIL_ERR_INVALID, "missing emitter array");
     HIP_TRY(hipSetDevice(pt->device));
-    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(order_after_renders(pt));
     pt->pipe_valid = false;
+    bool in_place = pt->d_areas && scene->num_area_emitters == pt->sc.num_areas && same_env(pt, scene);
+    for (uint32_t e = 0; in_place && e < scene->num_area_emitters; e++)
+        in_place = scene->area_emitters[e].radiance.type != PUPIL_TEX_BITMAP;
+    if (in_place) {
+        std::vector<DevEmitter> areas;
+        std::vector<float> cdf;
+        std::vector<uint32_t> guide;
+        uint32_t bits = 0;
+        if (const int rc = emitter_tables(pt, scene, areas, cdf, guide, bits)) return rc;
+        if (guide.empty() == (pt->d_guide != nullptr) || bits != pt->sc.guide_bits) in_place = false;
+        if (in_place) {
+            pt->h_emit_areas.swap(areas);  // kept alive until the copies have run (synchronised below)
+            pt->h_emit_cdf.swap(cdf);
+            pt->h_emit_guide.swap(guide);
+            HIP_TRY(hipMemcpyAsync(pt->d_areas, pt->h_emit_areas.data(), sizeof(DevEmitter) * pt->h_emit_areas.size(),
+                                   hipMemcpyHostToDevice, pt->own_stream));
+            HIP_TRY(hipMemcpyAsync(pt->d_cdf, pt->h_emit_cdf.data(), sizeof(float) * pt->h_emit_cdf.size(),
+                                   hipMemcpyHostToDevice, pt->own_stream));
+            if (pt->d_guide)
+                HIP_TRY(hipMemcpyAsync(pt->d_guide, pt->h_emit_guide.data(), sizeof(uint32_t) * pt->h_emit_guide.size(),
+                                       hipMemcpyHostToDevice, pt->own_stream));
+            HIP_TRY(hipStreamSynchronize(pt->own_stream));
+            return PUPIL_OK;
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(pt->own_stream));  // the old tables are freed below
     return upload_emitters(pt, scene);
 }
 
@@ -1009,7 +1149,10 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     // only the inspector clamps to 1..128): any depth renders.  Diagnostics sized per
     // bounce (tail buffer) cover the first kMaxDepth launches.
     const uint32_t depth = std::max(1u, launch->max_depth ? launch->max_depth : pt->max_depth);
-    if (pt->rendered && s != pt->last_stream) HIP_TRY(hipStreamWaitEvent(s, pt->ev_end, 0));
+    if (pt->rendered && s != pt->last_stream) {  // another stream: after everything the last one holds
+        HIP_TRY(hipEventRecord(pt->ev_sync, pt->last_stream));
+        HIP_TRY(hipStreamWaitEvent(s, pt->ev_sync, 0));
+    }
 
     FrameParams fp{};
     fp.width = pt->width;
@@ -1036,7 +1179,21 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     const bool trace_timing = (launch->collect_stats & PUPIL_STATS_TRACE_TIMING) != 0 && !timing;
     RenderCtx cx{pt, s, stats, timing || trace_timing, TraceStats{pt->trace_counters}, key};
     cx.trace_only = trace_timing;
-    cx.pair = trace_timing && pt->pairs_keep ? pt->trace_pairs : 0u;
+    if (!(trace_timing && pt->pairs_keep)) {  // a new sum
+        pt->trace_pairs = 0;
+        for (int k = 0; k < 3; k++) pt->kept_ms[k] = 0.0, pt->kept_n[k] = 0;
+    }
+    if (trace_timing && pt->trace_pairs >= kMaxPairs) {  // a long unread sequence: fold the pending pairs
+        HIP_TRY(hipEventSynchronize(pt->trace_events[2 * pt->trace_pairs - 1]));
+        for (uint32_t i = 0; i < pt->trace_pairs; i++) {
+            float m = 0.f;
+            HIP_TRY(hipEventElapsedTime(&m, pt->trace_events[2 * i], pt->trace_events[2 * i + 1]));
+            pt->kept_ms[pt->pair_kind[i]] += m;
+            pt->kept_n[pt->pair_kind[i]]++;
+        }
+        pt->trace_pairs = 0;
+    }
+    cx.pair = trace_timing ? pt->trace_pairs : 0u;
     pt->pairs_keep = trace_timing;
     const bool tail = stats && std::getenv("PUPIL_TRACE_TAIL");
     if (tail && !pt->tail_buf) {
@@ -1046,29 +1203,24 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     if (tail) HIP_TRY(hipMemsetAsync(pt->tail_buf, 0, sizeof(unsigned long long) * (kMaxDepth + 1) * pt->tail_waves * 4, s));
     cx.tail = tail;
     pt->tail_launches = 0;
-    const uint32_t iters = depth + 1;  // both schedules run at most depth iterations (+1 spare)
-    if (iters > pt->ray_log_cap) {
-        if (pt->ray_log) (void)hipFree(pt->ray_log);
-        pt->ray_log = nullptr;
-        pt->ray_log_cap = 0;
-        HIP_TRY(hipMalloc((void **)&pt->ray_log, sizeof(uint32_t) * 2 * iters));
-        pt->ray_log_cap = iters;
+    // events only when times are asked for: one pair per stage launch (kind 0 primary extend,
+    // 1 bounce trace, 2 shade), at most two stage launches per iteration and kMaxPairs in all
+    if (cx.timing) {
+        const uint64_t pairs_needed = std::min<uint64_t>((uint64_t)cx.pair + 2ull * depth + 1ull, kMaxPairs + 2ull * 64);
+        cx.pair_cap = (uint32_t)pairs_needed;
+        while (pt->trace_events.size() < 2 * pairs_needed) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            pt->trace_events.push_back(e);
+        }
+        if (pt->pair_kind.size() < pairs_needed) pt->pair_kind.resize(pairs_needed, 0);
     }
-    HIP_TRY(hipMemsetAsync(pt->ray_log, 0, sizeof(uint32_t) * 2 * iters, s));
-    // events: begin/end + one pair per stage launch (kind 0 primary extend, 1 bounce trace, 2 shade)
-    const uint32_t pairs_needed = cx.pair + 3 * depth + 1;
-    while (pt->trace_events.size() < 2 * pairs_needed) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreate(&e));
-        pt->trace_events.push_back(e);
-    }
-    pt->pair_kind.resize(pairs_needed, 0);
-
-    HIP_TRY(hipEventRecord(pt->ev_begin, s));
+    pt->last_timed = stats || timing;
+    if (pt->last_timed) HIP_TRY(hipEventRecord(pt->ev_begin, s));
     if (stats) HIP_TRY(hipMemsetAsync(pt->trace_counters, 0, 32 * sizeof(unsigned long long), s));
     const int rc = render_pipelined(cx, fp, launch);
     if (rc) return rc;
-    HIP_TRY(hipEventRecord(pt->ev_end, s));
+    if (pt->last_timed) HIP_TRY(hipEventRecord(pt->ev_end, s));
     HIP_TRY(hipGetLastError());
     pt->trace_pairs = cx.pair;
     pt->last_paths = fp.num_paths;
@@ -1081,35 +1233,30 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
 int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
     if (!pt || !out) return fail(PUPIL_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(pt->device));
-    HIP_TRY(hipEventSynchronize(pt->ev_end));
+    if (pt->rendered) HIP_TRY(hipStreamSynchronize(pt->last_stream));
     pupil_pt_counters c = pt->totals;
-    {
-        unsigned long long cum[2] = {0, 0};
-        HIP_TRY(hipMemcpy(cum, pt->ray_cum, sizeof(cum), hipMemcpyDeviceToHost));
-        c.rays_traced_total = pt->primary_cum + cum[0] + cum[1];
-        c.frames_in_flight = pt->pipe.size();
-        c.pipeline_slots = pt->pipe_slots;
-        c.tlas_sah_splits = pt->two_level ? pt->tl.sah_splits : 0u;
-    }
+    unsigned long long cum[4] = {0, 0, 0, 0};  // running totals, then their values before the last render
+    HIP_TRY(hipMemcpy(cum, pt->ray_cum, sizeof(cum), hipMemcpyDeviceToHost));
+    c.rays_traced_total = pt->primary_cum + cum[0] + cum[1];
+    c.frames_in_flight = pt->pipe.size();
+    c.pipeline_slots = pt->pipe_slots;
+    c.tlas_sah_splits = pt->two_level ? pt->tl.sah_splits : 0u;
+    c.ring_bytes = pt->ring_bytes + sizeof(float) * (uint64_t)pt->aov_cap;
+    c.ring_budget_bytes = (uint64_t)pt->pipe_budget;
+    c.accel_refits = pt->refits;
+    for (int a = 0; a < 3; a++) c.node_bound[a] = pt->sc.node_bound[a];
     if (pt->last_paths) {
         // rays traced by the last render's launches (pipelined renders: of every frame in
-        // flight; iteration 0 of a render that started on an empty pipeline logs none)
-        std::vector<uint32_t> log(2 * (size_t)pt->last_iters, 0);
-        if (!log.empty())
-            HIP_TRY(hipMemcpy(log.data(), pt->ray_log, sizeof(uint32_t) * log.size(), hipMemcpyDeviceToHost));
+        // flight; a render whose only iteration traced camera rays lists none)
         c.primary_rays = pt->last_primary;
         c.path_samples = pt->last_paths;
-        c.extension_rays = 0;
-        c.shadow_rays = 0;
-        for (uint32_t b = 0; b < pt->last_iters; b++) {
-            c.extension_rays += log[2 * b];
-            c.shadow_rays += log[2 * b + 1];
-        }
+        c.extension_rays = pt->snap_taken ? cum[0] - cum[2] : 0u;
+        c.shadow_rays = pt->snap_taken ? cum[1] - cum[3] : 0u;
         float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, pt->ev_begin, pt->ev_end));
+        if (pt->last_timed) HIP_TRY(hipEventElapsedTime(&ms, pt->ev_begin, pt->ev_end));
         c.last_render_ms = ms;
-        double kind_ms[3] = {0.0, 0.0, 0.0};
-        uint64_t kind_n[3] = {0, 0, 0};
+        double kind_ms[3] = {pt->kept_ms[0], pt->kept_ms[1], pt->kept_ms[2]};
+        uint64_t kind_n[3] = {pt->kept_n[0], pt->kept_n[1], pt->kept_n[2]};
         for (uint32_t i = 0; i < pt->trace_pairs; i++) {
             float m = 0.f;
             HIP_TRY(hipEventElapsedTime(&m, pt->trace_events[2 * i], pt->trace_events[2 * i + 1]));
@@ -1232,7 +1379,10 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
         pt->last_iters = 0;
         pt->last_primary = n;
         pt->last_stats = true;
+        pt->last_timed = true;
+        pt->snap_taken = false;
         pt->trace_pairs = 0;
+        for (int k = 0; k < 3; k++) pt->kept_ms[k] = 0.0, pt->kept_n[k] = 0;
         pt->rendered = true;
         pt->last_stream = pt->own_stream;
     }
@@ -1262,6 +1412,21 @@ int pupil_debug_select_emitter(pupil_pt *pt, uint32_t n, const float *p, int32_t
     if (dout) (void)hipFree(dout);
     HIP_TRY(err);
     return PUPIL_OK;
+}
+
+int pupil_debug_fill_tlas_reserve(pupil_pt *pt, float value) {
+    if (!pt) return fail(PUPIL_ERR_INVALID, "null argument");
+    if (!pt->two_level) return fail(PUPIL_ERR_UNSUPPORTED, "the flattened BVH has no TLAS reserve");
+    HIP_TRY(hipSetDevice(pt->device));
+    HIP_TRY(order_after_renders(pt));
+    const uint64_t lo = pt->tl.tlas_nodes, hi = std::min<uint64_t>(pt->tl.tlas_cap, nodes4_count(pt));
+    if (hi > lo) {
+        std::vector<float> junk((hi - lo) * (sizeof(Bvh4Node) / sizeof(float)), value);
+        HIP_TRY(hipMemcpyAsync((void *)(pt->sc.nodes4 + lo), junk.data(), sizeof(float) * junk.size(),
+                               hipMemcpyHostToDevice, pt->own_stream));
+        HIP_TRY(hipStreamSynchronize(pt->own_stream));
+    }
+    return refresh_node_bound(pt);
 }
 
 int pupil_debug_math(int device, uint32_t n, const float *x, const float *y2, float *out) {

@@ -214,10 +214,11 @@ void launch_debug_select(const DeviceScene &sc, const float *p, int *out, uint32
 // stable partition of path ids 0..n-1 by a key byte (queue_partition.hip)
 uint32_t partition_hist_entries(uint32_t n);
 // log_out (or null): the nbins counts; cum_out (or null): the counts are added to these
-// nbins running 64-bit totals (rays traced since the engine was created)
+// nbins running 64-bit totals (rays traced since the engine was created); snap_out (or
+// null): receives the totals as they were before this partition added to them
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
                       uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, uint32_t *log_out,
-                      hipStream_t s, unsigned long long *cum_out = nullptr);
+                      hipStream_t s, unsigned long long *cum_out = nullptr, unsigned long long *snap_out = nullptr);
 
 // LBVH builder (bvh_build.hip)
 struct BvhBuildInput {
@@ -247,10 +248,12 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
 int build_bvh_bounded(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size, hipStream_t s,
                       double *build_ms, uint32_t reserve);
 void free_lbvh(BvhBuildOutput &out);
-// RenderInstanceUpdate without a rebuild: the records of instance `moved` get its new
-// world vertices and every BVH4 node box is refitted bottom up (topology kept, like the
-// reference's IAS update).  Needs the breadth-first level order; -1 when unavailable.
-int refit_bvh4(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t moved, hipStream_t s, double *ms);
+// RenderInstanceUpdate without a rebuild: the records of the instances flagged in
+// `moved` (device, one byte per instance) get their new world vertices and every BVH4 node
+// box is refitted bottom up (topology kept, like the reference's IAS update); nbox: device
+// scratch of 6 floats per node.  Needs the breadth-first level order; -1 when unavailable.
+int refit_bvh4(const BvhBuildInput &in, BvhBuildOutput &out, const uint8_t *moved, float *nbox, hipStream_t s,
+               double *ms);
 // BVH4 over n >= 2 boxes (6 floats each: lo xyz, hi xyz) with the flattened build's PLOC +
 // SAH collapse, one box per leaf: nodes (root 0, parents first) and, for leaf link
 // make_leaf(p, 1), the box order[p]; depth = 4-wide levels

@@ -104,7 +104,7 @@ constexpr uint32_t kScanChunk = 1024u * kScanPer;
 __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nblk, uint32_t nbins,
                                                     uint32_t *counts_out, uint32_t *starts_out,
                                                     uint32_t *total_out, uint32_t *log_out,
-                                                    unsigned long long *cum_out) {
+                                                    unsigned long long *cum_out, unsigned long long *snap_out) {
     __shared__ uint32_t sh[kScanChunk];
     __shared__ uint32_t wave_sum[16];
     __shared__ uint32_t carry_s;
@@ -164,6 +164,7 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nbl
         starts_out[t] = start;
         counts_out[t] = next - start;
         if (log_out) log_out[t] = next - start;
+        if (snap_out) snap_out[t] = cum_out[t];  // the totals before this partition
         if (cum_out) cum_out[t] += next - start;  // one block, stream-ordered: no atomics needed
     }
     if (t == 0 && total_out) *total_out = carry;
@@ -212,7 +213,7 @@ uint32_t partition_hist_entries(uint32_t n) {
 
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
                       uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, uint32_t *log_out,
-                      hipStream_t s, unsigned long long *cum_out) {
+                      hipStream_t s, unsigned long long *cum_out, unsigned long long *snap_out) {
     const uint32_t nblk = part_blocks(n);
     const uint32_t rounds = part_rounds(n);
     if (nblk == 0) {
@@ -220,13 +221,15 @@ void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode 
         (void)hipMemsetAsync(starts_out, 0, sizeof(uint32_t) * nbins, s);
         if (total_out) (void)hipMemsetAsync(total_out, 0, sizeof(uint32_t), s);
         if (log_out) (void)hipMemsetAsync(log_out, 0, sizeof(uint32_t) * nbins, s);
+        if (snap_out && cum_out)
+            (void)hipMemcpyAsync(snap_out, cum_out, sizeof(unsigned long long) * nbins, hipMemcpyDeviceToDevice, s);
         return;
     }
 #define PART_RUN(M)                                                                                                \
     hipLaunchKernelGGL(k_part_count<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk,      \
                        rounds);                                                                                    \
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, hist, nblk, nbins, counts_out, starts_out,          \
-                       total_out, log_out, cum_out);                                                                        \
+                       total_out, log_out, cum_out, snap_out);                                                                      \
     hipLaunchKernelGGL(k_part_scatter<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk, out, \
                        rounds)
     switch (mode) {

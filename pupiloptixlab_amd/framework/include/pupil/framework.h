@@ -22,7 +22,9 @@
 #include <mutex>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <vector>
+#include <atomic>
 
 #include "../../../../include/pupil_pt.h"
 #include "dist.h"
@@ -146,10 +148,21 @@ public:
     void Init(bool has_window = false) noexcept;  // headless; has_window is accepted and ignored
     void AddPass(Pass *pass) noexcept;
     // Loads a mitsuba XML scene (resource/scene.cpp subset), allocates the
-    // "final result" buffer and fires ESystemEvent::SceneLoad with the World.
+    // "final result" buffer and fires ESystemEvent::SceneLoad with the World --
+    // under the render mutex, as system.cpp:142-165 does, so no frame is in flight.
     bool SetScene(const std::filesystem::path &xml) noexcept;
     bool SetScene(std::unique_ptr<world::World> world) noexcept;  // programmatic scenes
-    void Run(uint32_t frames) noexcept;  // every enabled pass, `frames` times
+    // `frames` frames on the caller's thread, each under the render mutex
+    void Run(uint32_t frames) noexcept;
+    // The reference's render thread (system.cpp:93-106): a thread that renders frames
+    // (every enabled pass, then ESystemEvent::FrameFinished) under the render mutex
+    // until Stop() or Destroy().  Other threads meanwhile fire events (a camera move,
+    // RenderInstanceUpdate), which the passes pick up at the top of their next OnRun.
+    void RunAsync() noexcept;
+    void Stop() noexcept;
+    uint64_t FramesRendered() const noexcept { return m_frames.load(); }
+    // Holds off the render thread (e.g. to apply several scene edits as one change).
+    std::unique_lock<std::mutex> RenderLock() noexcept;
     void Destroy() noexcept;
     world::World *GetWorld() noexcept { return m_world.get(); }
 
@@ -161,9 +174,16 @@ public:
     FrameGather *Gather() noexcept { return m_gather.get(); }
 
 private:
+    void RenderFrame() noexcept;  // caller holds m_render_system_mutex
+
     std::vector<Pass *> m_passes;
     std::unique_ptr<world::World> m_world;
     std::unique_ptr<FrameGather> m_gather;
+    std::mutex m_render_system_mutex;
+    std::thread m_render_thread;
+    std::atomic_bool m_quit{false};
+    std::atomic<uint64_t> m_frames{0};
+    std::atomic<int> m_lock_waiters{0};  // RenderLock callers: the render thread lets them in first
 };
 
 }  // namespace Pupil

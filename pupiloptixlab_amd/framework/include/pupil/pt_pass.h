@@ -6,7 +6,9 @@
 #pragma once
 
 #include <atomic>
+#include <mutex>
 #include <string_view>
+#include <vector>
 
 #include "framework.h"
 #include "world.h"
@@ -43,6 +45,10 @@ private:
     int m_max_depth = 1;
     bool m_accumulated_flag = true;
     std::atomic_bool m_dirty = true;
+    // instances moved since the last OnRun (RenderInstanceUpdate only records them, as the
+    // reference's handler only sets m_dirty, pt_pass.cpp:216-218; OnRun refits once)
+    std::mutex m_pending_mutex;
+    std::vector<uint32_t> m_pending;
 };
 
 }  // namespace Pupil::pt

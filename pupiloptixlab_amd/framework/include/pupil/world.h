@@ -25,14 +25,19 @@ struct SceneInfo {
 
 class CameraHelper {
 public:
+    // Unsynchronised views (single-threaded use); a render thread takes Snapshot().
     const float *SampleToCamera() const noexcept { return m_s2c; }
     const float *CameraToWorld() const noexcept { return m_c2w; }
     // Replace the camera-to-world matrix (row-major 4x4) and fire
     // EWorldEvent::CameraChange, like CameraHelper's setters (world/camera.cpp).
+    // Safe from any thread (the World's mutex guards the matrices).
     void SetCameraToWorld(const float c2w[16]) noexcept;
+    void Snapshot(float s2c[16], float c2w[16]) const noexcept;
     void Load(const pupil_scene_desc &d) noexcept;
 
 private:
+    friend class World;
+    std::mutex *m_lock = nullptr;  // the owning World's mutex
     float m_s2c[16] = {};
     float m_c2w[16] = {};
 };
@@ -58,16 +63,20 @@ public:
     // Programmatic scenes: the caller filled `handle()` through pupil_world_*.
     bool Finalize() noexcept;
     // Moves instance `instance` (row-major 4x4), refreshes Desc() (instance
-    // matrices, area emitters) and fires EWorldEvent::RenderInstanceUpdate.
+    // matrices, area emitters) and fires EWorldEvent::RenderInstanceUpdate.  Safe from
+    // any thread: the edit happens under Mutex(), the event is fired after it.
     bool SetInstanceTransform(uint32_t instance, const float to_world[16]) noexcept;
 
     pupil_world *handle() noexcept { return m_world; }
-    // Flattened scene for pupil_pt_create (valid until the world changes).
+    // Flattened scene for pupil_pt_create (valid until the world changes); a thread
+    // reading it while another may edit the world holds Mutex().
     const pupil_scene_desc &Desc() const noexcept { return m_desc; }
+    std::mutex &Mutex() noexcept { return m_mutex; }
 
 private:
     pupil_world *m_world = nullptr;
     pupil_scene_desc m_desc{};
+    std::mutex m_mutex;
 };
 
 }  // namespace Pupil::world

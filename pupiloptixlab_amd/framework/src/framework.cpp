@@ -110,6 +110,7 @@ bool System::InitDistributed(const DistInfo &d) noexcept {
 
 bool System::SetScene(std::unique_ptr<world::World> w) noexcept {
     if (!w) return false;
+    std::scoped_lock render_lock(m_render_system_mutex);  // system.cpp:145
     (void)hipSetDevice(device);
     if (m_gather && !m_gather->Setup((uint32_t)w->scene->sensor.film.w, (uint32_t)w->scene->sensor.film.h)) {
         Log("tile maps for the multi-GPU gather could not be set up");
@@ -127,14 +128,53 @@ bool System::SetScene(std::unique_ptr<world::World> w) noexcept {
     return true;
 }
 
+void System::RenderFrame() noexcept {
+    for (Pass *p : m_passes) p->Run();
+    m_frames++;
+}
+
 void System::Run(uint32_t frames) noexcept {
+    (void)hipSetDevice(device);
     for (uint32_t f = 0; f < frames; f++) {
-        for (Pass *p : m_passes) p->Run();
+        {
+            std::scoped_lock render_lock(m_render_system_mutex);
+            RenderFrame();
+        }
         EventDispatcher<ESystemEvent::FrameFinished>();
     }
 }
 
+void System::RunAsync() noexcept {
+    if (m_render_thread.joinable()) return;
+    m_quit = false;
+    m_render_thread = std::thread([this] {
+        (void)hipSetDevice(device);  // HIP's current device is per thread
+        while (!m_quit) {
+            while (m_lock_waiters.load() > 0 && !m_quit) std::this_thread::yield();  // no starvation
+            {
+                std::scoped_lock render_lock(m_render_system_mutex);
+                if (m_quit) break;
+                RenderFrame();
+            }
+            EventDispatcher<ESystemEvent::FrameFinished>();
+        }
+    });
+}
+
+std::unique_lock<std::mutex> System::RenderLock() noexcept {
+    m_lock_waiters++;
+    std::unique_lock<std::mutex> lock(m_render_system_mutex);
+    m_lock_waiters--;
+    return lock;
+}
+
+void System::Stop() noexcept {
+    m_quit = true;
+    if (m_render_thread.joinable()) m_render_thread.join();
+}
+
 void System::Destroy() noexcept {
+    Stop();
     EventDispatcher<ESystemEvent::Quit>();
     m_passes.clear();
     m_world.reset();

@@ -2,6 +2,7 @@
 #include "pupil/pt_pass.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace Pupil::pt {
 
@@ -18,16 +19,41 @@ PTPass::~PTPass() noexcept {
     if (m_stream) (void)hipStreamDestroy(m_stream);
 }
 
-// pt_pass.cpp:39-57: refresh on dirty (camera, depth, accumulation reset),
-// one 1-spp frame, synchronise, advance seed and sample count.
+// pt_pass.cpp:39-57: refresh on dirty (camera, instances moved since the last frame,
+// depth, accumulation reset), one 1-spp frame, synchronise, advance seed and sample
+// count.  Runs on the render thread; events may arrive from any other thread.
 void PTPass::OnRun() noexcept {
     if (!m_engine) return;
     if (m_dirty) {
-        pupil_pt_set_camera(m_engine, m_world->camera->SampleToCamera(), m_world->camera->CameraToWorld());
+        m_dirty = false;  // an event after this point marks the next frame dirty again
+        std::vector<uint32_t> moved;
+        {
+            std::scoped_lock lock(m_pending_mutex);
+            moved.swap(m_pending);
+        }
+        float s2c[16], c2w[16];
+        m_world->camera->Snapshot(s2c, c2w);
+        pupil_pt_set_camera(m_engine, s2c, c2w);
+        if (!moved.empty()) {  // m_world->GetIASHandle(2, true) + the emitter group (pt_pass.cpp:46-47)
+            std::scoped_lock lock(m_world->Mutex());
+            const pupil_scene_desc &d = m_world->Desc();
+            std::vector<float> tw(12 * moved.size()), to(12 * moved.size());
+            bool emissive = false;
+            for (size_t k = 0; k < moved.size(); k++) {
+                const pupil_instance &ins = d.instances[moved[k]];
+                std::memcpy(&tw[12 * k], ins.to_world, sizeof(ins.to_world));
+                std::memcpy(&to[12 * k], ins.to_object, sizeof(ins.to_object));
+                emissive = emissive || ins.emitter_offset >= 0;
+            }
+            if (pupil_pt_update_instances(m_engine, (uint32_t)moved.size(), moved.data(), tw.data(), to.data()) !=
+                PUPIL_OK)
+                Log("%s: instance update failed: %s", name.c_str(), pupil_last_error());
+            else if (emissive && pupil_pt_update_emitters(m_engine, &d) != PUPIL_OK)
+                Log("%s: emitter update failed: %s", name.c_str(), pupil_last_error());
+        }
         m_frame_max_depth = (uint32_t)m_max_depth;
         m_sample_cnt = 0;
         m_random_seed = 0;
-        m_dirty = false;
     }
     pupil_pt_launch launch{};
     launch.random_seed = m_random_seed;
@@ -57,6 +83,10 @@ void PTPass::OnRun() noexcept {
 void PTPass::SetScene(world::World *world) noexcept {
     if (!world) return;
     m_world = world;
+    {
+        std::scoped_lock lock(m_pending_mutex);  // moves of the previous world
+        m_pending.clear();
+    }
     if (m_engine) {
         pupil_pt_destroy(m_engine);
         m_engine = nullptr;
@@ -129,14 +159,13 @@ bool PTPass::Stats(pupil_pt_counters &out) noexcept { return m_engine && pupil_p
 void PTPass::BindingEventCallback() noexcept {
     EventBinder<EWorldEvent::CameraChange>([this](void *) { m_dirty = true; });
     EventBinder<EWorldEvent::RenderInstanceUpdate>([this](void *p) {
-        // IAS update + emitter reset (ias_manager.cpp:116-151, world.cpp:45-54), then restart accumulation
+        // only recorded: the next OnRun refits once for every instance moved since the last
+        // (ias_manager.cpp:116-151, world.cpp:45-54) and restarts accumulation
         const auto *u = static_cast<const world::InstanceUpdate *>(p);
-        if (u && u->world == m_world && m_engine) {
-            const pupil_instance &ins = m_world->Desc().instances[u->instance];
-            if (pupil_pt_update_instance(m_engine, u->instance, ins.to_world, ins.to_object) != PUPIL_OK)
-                Log("%s: instance update failed: %s", name.c_str(), pupil_last_error());
-            else if (ins.emitter_offset >= 0 && pupil_pt_update_emitters(m_engine, &m_world->Desc()) != PUPIL_OK)
-                Log("%s: emitter update failed: %s", name.c_str(), pupil_last_error());
+        if (u && u->world == m_world) {
+            std::scoped_lock lock(m_pending_mutex);
+            if (std::find(m_pending.begin(), m_pending.end(), u->instance) == m_pending.end())
+                m_pending.push_back(u->instance);
         }
         m_dirty = true;
     });

@@ -11,8 +11,19 @@ void CameraHelper::Load(const pupil_scene_desc &d) noexcept {
 }
 
 void CameraHelper::SetCameraToWorld(const float c2w[16]) noexcept {
-    std::memcpy(m_c2w, c2w, sizeof(m_c2w));
+    {
+        std::unique_lock<std::mutex> lock;
+        if (m_lock) lock = std::unique_lock<std::mutex>(*m_lock);
+        std::memcpy(m_c2w, c2w, sizeof(m_c2w));
+    }
     EventDispatcher<EWorldEvent::CameraChange>(this);
+}
+
+void CameraHelper::Snapshot(float s2c[16], float c2w[16]) const noexcept {
+    std::unique_lock<std::mutex> lock;
+    if (m_lock) lock = std::unique_lock<std::mutex>(*m_lock);
+    std::memcpy(s2c, m_s2c, sizeof(m_s2c));
+    std::memcpy(c2w, m_c2w, sizeof(m_c2w));
 }
 
 World::World() noexcept {
@@ -22,6 +33,7 @@ World::World() noexcept {
     }
     scene = std::make_unique<SceneInfo>();
     camera = std::make_unique<CameraHelper>();
+    camera->m_lock = &m_mutex;
 }
 
 World::~World() noexcept {
@@ -50,11 +62,18 @@ bool World::Finalize() noexcept {
 }
 
 bool World::SetInstanceTransform(uint32_t instance, const float to_world[16]) noexcept {
-    if (!m_world || pupil_world_set_instance_transform(m_world, instance, to_world) != PUPIL_OK) {
-        Log("instance update failed: %s", pupil_last_error());
-        return false;
+    {
+        std::scoped_lock lock(m_mutex);
+        if (!m_world || pupil_world_set_instance_transform(m_world, instance, to_world) != PUPIL_OK) {
+            Log("instance update failed: %s", pupil_last_error());
+            return false;
+        }
+        // the desc only: the camera keeps any SetCameraToWorld made since the load
+        if (pupil_world_get_desc(m_world, &m_desc) != PUPIL_OK) {
+            Log("scene description failed: %s", pupil_last_error());
+            return false;
+        }
     }
-    if (!Finalize()) return false;
     InstanceUpdate u{this, instance};
     EventDispatcher<EWorldEvent::RenderInstanceUpdate>(&u);
     return true;

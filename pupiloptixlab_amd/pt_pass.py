@@ -102,25 +102,43 @@ class PTPass(Pass):
         self.dirty = True
         self.tile = (32, 0, 1)  # tile_size, rank, world
         self._world = None  # the World the scene came from: its sensor is re-read when dirty
+        self._pending = {}  # RenderInstanceUpdate events since the last render: id(world) -> (world, instances)
         self.events = events or Events()
         self.events.bind(Events.CAMERA_CHANGE, lambda _: self.mark_dirty())
         self.events.bind(Events.RENDER_INSTANCE_UPDATE, self._on_instance_update)
         self.events.bind(Events.SCENE_LOAD, lambda w: self.set_scene(w))
 
     def _on_instance_update(self, arg):
+        """RenderInstanceUpdate handler: only records the moved instance and marks the pass
+        dirty, like the reference's (pt_pass.cpp:216-218); the next render refits once
+        for every instance recorded since the last one (GetIASHandle(2, true), :46)."""
         if arg is not None:
-            self.update_instance(*arg)
-        else:
-            self.mark_dirty()
+            world, instance = arg
+            self._pending.setdefault(id(world), (world, set()))[1].add(int(instance))
+        self.mark_dirty()
 
     def update_instance(self, world, instance: int):
-        """RenderInstanceUpdate: push instance `instance`'s new transform from `world`
-        (already moved with World.set_instance_transform) into the engine, and the
+        """RenderInstanceUpdate applied now: push instance `instance`'s new transform from
+        `world` (already moved with World.set_instance_transform) into the engine, and the
         emitter table when the instance is emissive; restarts accumulation."""
+        self.update_instances(world, [instance])
+
+    def update_instances(self, world, instances):
+        """Several moved instances with ONE refit of the acceleration structure
+        (pupil_pt_update_instances), then the emitter table if any of them emits."""
+        import numpy as np
+
+        ids = sorted({int(i) for i in instances})
+        if not ids:
+            return
         desc = world.desc()
-        ins = desc.instances[instance]
-        check(self._lib.pupil_pt_update_instance(self._pt, int(instance), ins.to_world, ins.to_object))
-        if ins.emitter_offset >= 0:
+        tw = np.array([list(desc.instances[i].to_world) for i in ids], np.float32)
+        to = np.array([list(desc.instances[i].to_object) for i in ids], np.float32)
+        idv = np.array(ids, np.uint32)
+        check(self._lib.pupil_pt_update_instances(self._pt, len(ids), idv.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                  tw.ctypes.data_as(C.POINTER(C.c_float)),
+                                                  to.ctypes.data_as(C.POINTER(C.c_float))))
+        if any(desc.instances[i].emitter_offset >= 0 for i in ids):
             check(self._lib.pupil_pt_update_emitters(self._pt, C.byref(desc)))
         self.dirty = True
 
@@ -175,6 +193,7 @@ class PTPass(Pass):
         desc = world.desc() if hasattr(world, "desc") else world
         self._world = world if hasattr(world, "desc") else None
         self.close_engine()
+        self._pending = {}
         self._torch.cuda.set_device(self.device_index)
         check(self._lib.pupil_pt_create(C.byref(desc), self.device_index, C.byref(self._pt)))
         self.width, self.height = desc.width, desc.height
@@ -212,7 +231,10 @@ class PTPass(Pass):
         continues: the next render() continues this one (progressive rendering), so the
         engine traces its camera rays ahead (PUPIL_HINT_CONTINUE; single-spp renders
         always do)."""
-        if self.dirty:  # pt_pass.cpp:40-49: camera re-uploaded, accumulation restarted
+        if self.dirty:  # pt_pass.cpp:40-49: camera re-uploaded, instances refitted, accumulation restarted
+            pending, self._pending = self._pending, {}
+            for world, ids in pending.values():
+                self.update_instances(world, ids)
             if self._world is not None:
                 d = self._world.desc()
                 check(self._lib.pupil_pt_set_camera(self._pt, d.sample_to_camera, d.camera_to_world))

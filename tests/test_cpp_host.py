@@ -202,3 +202,39 @@ def test_rccl_id_path_agrees_across_differently_started_ranks():
     env["TORCHELASTIC_RUN_ID"] = "r2"
     other = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
     assert other.stdout.strip() != direct.stdout.strip()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("instance", [5, 7])
+def test_example_render_thread_updates_match_oracle(instance, tmp_path):
+    """The reference's threading contract (system.cpp:93-106, pt_pass.cpp:39-57,216-218):
+    System::RunAsync renders on its own thread while the main thread, three times, takes
+    the render lock, moves one instance 4 times (RenderInstanceUpdate events) and the
+    camera (CameraChange).  PTPass only records the moves and refits once at the top of its
+    next OnRun: 12 updates cost 3 refits.  The frames accumulated since the last change
+    equal the oracle's render of the final state bit for bit.  Instance 7 is the Cornell
+    box's area light (its emitter table is rewritten in place as well)."""
+    _built()
+    import json
+
+    import oracle
+    from pupiloptixlab_amd import World, scenes
+
+    os.makedirs(TMP, exist_ok=True)
+    xml = scenes.cornell_xml(os.path.join(TMP, "cb_thread.xml"), 64, 48, 4)
+    accum = str(tmp_path / "accum.f32")
+    env = dict(os.environ, PUPIL_THREAD_TEST=f"4,3,{instance}", PUPIL_BENCH_ACCUM=accum)
+    r = subprocess.run([EXE, xml], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["updates"] == 12 and rec["accel_refits"] == 3, rec
+    n = rec["frames_accumulated"]
+    assert n >= 2 and rec["frames_rendered"] > n
+    w = World().load_scene(xml)
+    w.set_instance_transform(instance, np.array(rec["to_world"], np.float32).reshape(4, 4))
+    desc = w.desc()
+    desc.camera_to_world[:] = [float(x) for x in rec["camera_to_world"]]
+    ref = oracle.OracleScene(desc).render(spp=n)["accum"]
+    got = np.fromfile(accum, np.float32).reshape(-1, 4)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), \
+        f"{(got.view(np.uint32) != ref.view(np.uint32)).any(axis=1).sum()} pixels differ"

@@ -645,6 +645,112 @@ def test_max_depth_above_128_renders():
         (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
 
 
+def test_huge_max_depth_renders_and_stops_early():
+    """max_depth = 2^32 - 1 (the ABI takes any depth): the host neither wraps
+    its iteration arithmetic nor creates events per bounce, and it stops issuing bounces
+    once every path has terminated (the list lengths are read back every 16 iterations
+    above depth 64).  The image equals the oracle's render at the same depth."""
+    import time
+
+    w = World().load_scene(scenes.cornell_xml(os.path.join(TMP, "cb24dmax.xml"), 24, 24, 4))
+    desc = w.desc()
+    desc.max_depth = 0xFFFFFFFF
+    t0 = time.perf_counter()
+    gpu = render_gpu(desc, 2)
+    assert time.perf_counter() - t0 < 60
+    ref = oracle.OracleScene(desc).render(spp=2)
+    assert np.array_equal(gpu["pt accum buffer"].view(np.uint32), ref["accum"].view(np.uint32))
+    s, rs = gpu["stats"], ref["stats"]
+    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
+        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
+
+
+def test_coalesced_instance_updates_cost_one_refit():
+    """RenderInstanceUpdate events only record the moved instances (pt_pass.cpp:216-218);
+    the next render refits once for all of them: 5 events on 3 instances -> one refit,
+    and the render equals a fresh engine's and the oracle's for the moved scene."""
+    import torch
+    from pupiloptixlab_amd.pt_pass import Events, PTPass
+
+    w = scenes.sphere_field(8, 64, 48, 4, seed=5, merge=False)
+    n = w.desc().num_instances
+    pt = PTPass(device=0)
+    pt.set_scene(w)
+    pt.render(1)
+    r0 = pt.stats()["accel_refits"]
+    moves = [(2, (0.5, 1.0, 0.0)), (3, (1.0, 5.0, -2.0)), (2, (0.7, 1.2, 0.1)), (n - 1, (1.5, 13.5, -1.0)),
+             (3, (1.1, 5.1, -2.2))]
+    for inst, t in moves:
+        w.set_instance_transform(inst, world_mod.transform(rotate=((0, 1, 0), 15), translate=t))
+        pt.events.dispatch(Events.RENDER_INSTANCE_UPDATE, (w, inst))
+    assert pt.stats()["accel_refits"] == r0  # nothing done until the next render
+    pt.render(2)
+    torch.cuda.synchronize()
+    assert pt.stats()["accel_refits"] == r0 + 1
+    moved = pt.buffers.get("pt accum buffer").cpu().numpy()
+    pt.close_engine()
+    desc1 = w.desc()
+    assert np.array_equal(moved, render_gpu(desc1, 2)["pt accum buffer"])
+    ref = oracle.OracleScene(desc1).render(spp=2)["accum"]
+    assert np.array_equal(moved.view(np.uint32), ref.view(np.uint32))
+
+
+def test_tlas_reserve_contents_do_not_move_the_node_bound(monkeypatch):
+    """The slab-test bound is taken over live BVH4 nodes only: junk (huge, inf, NaN) in the
+    never-written TLAS reserve of the two-level node array leaves it unchanged (ADVICE r03:
+    leftover allocator contents used to loosen every ray's box test)."""
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    monkeypatch.setenv("PUPIL_ACCEL", "two_level")
+    w = scenes.instanced_field(num_instances=6, width=32, height=18, max_depth=4, seed=3, spheres_per_blas=10)
+    pt = PTPass(device=0)
+    pt.set_scene(w.desc())
+    b0 = pt.stats()["node_bound"]
+    assert all(np.isfinite(b0)) and max(b0) > 0
+    for junk in (1e30, float("inf"), float("nan")):
+        abi.check(pt._lib.pupil_debug_fill_tlas_reserve(pt._pt, junk))
+        assert pt.stats()["node_bound"] == b0, junk
+    pt.close_engine()
+
+
+def test_moving_camera_cadence_starts_no_frames_ahead():
+    """The OnRun cadence with a camera change before every OnRun (interactive use): no
+    render continues the previous one, so none starts frames ahead (they would be
+    discarded) and every traced ray belongs to a displayed frame; once the camera stops,
+    continued OnRuns pipeline again.  Every frame equals the oracle's."""
+    import torch
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    w = _cornell(48, depth=5)
+    desc = w.desc()
+    c2w0 = np.array(list(desc.camera_to_world), np.float32)
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    lib = pt._lib
+    for k in range(4):
+        c2w = c2w0.copy()
+        c2w[3] += 0.01 * k
+        abi.check(lib.pupil_pt_set_camera(pt._pt, desc.sample_to_camera, c2w.ctypes.data_as(abi.f32p)))
+        pt.dirty = False
+        pt.random_seed = pt.sample_cnt = 0
+        t0 = pt.stats()["rays_traced_total"]
+        pt.render(1)
+        torch.cuda.synchronize()
+        c = pt.stats()
+        assert c["frames_in_flight"] == 0, k
+        assert c["rays_traced_total"] - t0 == c["primary_rays"] + c["extension_rays"] + c["shadow_rays"]
+        d = World().load_scene(scenes.cornell_xml(os.path.join(TMP, "cb48d5.xml"), 48, 48, 5)).desc()
+        d.camera_to_world[:] = [float(x) for x in c2w]
+        ref = oracle.OracleScene(d).render(spp=1)["accum"]
+        got = pt.buffers.get("pt accum buffer").cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+    for _ in range(3):  # the camera stops: the OnRuns continue each other and pipeline
+        pt.render(1)
+    torch.cuda.synchronize()
+    assert pt.stats()["frames_in_flight"] > 0
+    pt.close_engine()
+
+
 def test_render_orders_with_torch_default_stream():
     """A render enqueued on torch's default stream (handle NULL) runs on that stream: a
     read on the same stream right after it, with no device synchronisation, sees the
