@@ -242,7 +242,8 @@ def main(argv=None):
     c1 = pt.stats()
     rays_local = c1["rays_traced_total"] - c0["rays_traced_total"]
     timed = {"trace_ms": c1["trace_ms"], "launches": c1["trace_launches"], "rays": rays_local,
-             "frames_in_flight": c1["frames_in_flight"], "pipeline_slots": c1["pipeline_slots"]}
+             "frames_in_flight": c1["frames_in_flight"], "pipeline_slots": c1["pipeline_slots"],
+             "ring_bytes": c1["ring_bytes"], "ring_budget_bytes": c1["ring_budget_bytes"]}
     # the last timed frame (seeds 0 .. seed_t0 + steps*spp - 1 accumulated), checked below
     last_accum = pt.buffers.get("pt accum buffer").clone() if rank == 0 and world == 1 else None
     last_frame = None
@@ -340,7 +341,9 @@ def main(argv=None):
                                 "returns; value counts exactly the rays the timed steps' launches traced)",
                        "pipeline": {"slots": int(timed["pipeline_slots"]),
                                     "frames_in_flight_after": int(timed["frames_in_flight"]),
-                                    "traversal_launches_timed": int(timed["launches"])},
+                                    "traversal_launches_timed": int(timed["launches"]),
+                                    "ring_gb": round(timed["ring_bytes"] / 1e9, 3),
+                                    "ring_budget_gb": round(timed["ring_budget_bytes"] / 1e9, 3)},
                        "rays_traced_plain_process": int(rays_plain_process),
                        "parallelism": f"tiles{args.tile}x{world}",
                        "area_emitters": int(desc.num_area_emitters),

@@ -934,6 +934,11 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (const char *fr = std::getenv("PUPIL_FRESH_SHADE")) pt->fresh_shade = std::atoi(fr) != 0;
     if (const char *a = std::getenv("PUPIL_AHEAD")) pt->ahead_mode = std::min(2, std::max(0, std::atoi(a)));
     if (const char *k = std::getenv("PUPIL_PIPE")) pt->pipe_limit = (uint32_t)std::min(63, std::max(0, std::atoi(k)));
+    {  // ring budget: a quarter of the device memory free now (after the scene and its BVH)
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+        pt->pipe_budget = 0.25 * (double)free_b;
+    }
     if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
     if (const char *g = std::getenv("PUPIL_PIPE_PATHS")) pt->pipe_paths = std::max(1.0, std::atof(g));
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
