@@ -470,7 +470,10 @@ struct HitGeo {
 // __closesthit__default (main.cu:216-230) + Geometry::GetHitLocalGeometry
 // (render/geometry.h:272-320), from the compact hit record and the primitive's
 // shading record (bvh_build.hip k_attrs: object-space vertices, normals, uvs).
-__device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, vec3 ro, vec3 rd, vec2 stale_uv) {
+// ro_rec: the ray origin record, read only for a sphere hit (the triangle position is
+// interpolated from the vertices)
+__device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, const float4 *ro_rec, vec3 rd,
+                                             vec2 stale_uv) {
     HitGeo out;
     const uint32_t idx = __float_as_uint(h.w);
     // flat: idx = record in traversal order, which names the instance; two-level:
@@ -508,6 +511,7 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, v
     g.texcoord = stale_uv;
     uint32_t local = 0;
     if (sphere) {
+        const vec3 ro = f3(ld_ps(ro_rec));
         g.position = ro + h.x * rd;
         const vec3 local_pos = xform_point(in.to_object, g.position);
         g.texcoord = sphere_texcoord(normalize(local_pos - v3(0.f)));
@@ -599,9 +603,8 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
                                               uint32_t p, bool fresh, uint32_t fresh_rng) {
     bool push_next = false, push_shadow = false;
     const float4 h = ld_ps(ps.hit + p);
-    const float4 o4 = ld_ps(ps.ray_o + p);
     const float4 d4 = ld_ps(ps.ray_d + p);
-    const vec3 ray_o = f3(o4), ray_d = f3(d4);
+    const vec3 ray_d = f3(d4);
     const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ld_ps(ps.misc + p);
     uint32_t rng = misc.x;
     const uint32_t flags = misc.y;
@@ -609,11 +612,12 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     float4 thr4 = fresh ? make_float4(1.f, 1.f, 1.f, 0.f) : ld_ps(ps.thr + p);
     vec3 T = f3(thr4);
     const float prev_pdf = thr4.w;
-    float4 rad4 = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ld_ps(ps.rad + p);
-    vec3 L = f3(rad4);
+    // the radiance record is read only when this hit adds emission (at most one addition per
+    // shade, so L + X is the same sum whenever it is formed): most shades never touch it
+    vec3 L_add = v3(0.f);
     const vec2 stale_uv = v2(__uint_as_float(misc.z), __uint_as_float(misc.w));
 
-    HitGeo hg = reconstruct(sc, h, ray_o, ray_d, stale_uv);
+    HitGeo hg = reconstruct(sc, h, ps.ray_o + p, ray_d, stale_uv);
     const DevInstance &in = sc.instances[hg.inst];
     const DevMaterial &mat = sc.materials[in.material];
     if (mat.twosided && dot(-ray_d, hg.g.normal) < 0.f) hg.g.normal = -hg.g.normal;  // geometry.h:316-320
@@ -625,7 +629,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     bool L_changed = fresh;  // rad is rewritten only when this hit adds emission (or was never stored)
     if (bounce == 0) {
         if (hg.emitter >= 0) {  // main.cu:88-92
-            L = L + emitter_radiance(sc.areas[hg.emitter], geo.texcoord);
+            L_add = emitter_radiance(sc.areas[hg.emitter], geo.texcoord);
             L_changed = true;
         }
         const float test = rng_next(rng);                                                    // main.cu:101
@@ -649,10 +653,10 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         const DevEmitter &e = sc.areas[hg.emitter];
         vec3 Le;
         float pdf_e;
-        emitter_eval_area(e, geo, ray_o, Le, pdf_e);
+        emitter_eval_area(e, geo, f3(ld_ps(ps.ray_o + p)), Le, pdf_e);
         if (!is_zero(pdf_e)) {
             const float mis = (flags >> 31) ? 1.f : mis_weight(prev_pdf, pdf_e * e.select_probability);
-            L = L + T * Le * mis;
+            L_add = T * Le * mis;
             L_changed = true;
         }
     }
@@ -727,10 +731,17 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         st_ps(ps.misc + p, make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
                                 __float_as_uint(geo.texcoord.y)));
     }
-    if (L_changed) st_ps(ps.rad + p, f4(L, 0.f));
+    if (L_changed) {
+        const vec3 L = f3(fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ld_ps(ps.rad + p)) + L_add;
+        st_ps(ps.rad + p, f4(L, 0.f));
+    }
 #else
+    {
+        vec3 L = f3(fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ld_ps(ps.rad + p));
+        if (L_changed) L = L + L_add;
+        st_ps(ps.rad + p, f4(L, 0.f));
+    }
     st_ps(ps.thr + p, f4(T, pdf_b));
-    st_ps(ps.rad + p, f4(L, 0.f));
     st_ps(ps.misc + p, make_uint4(rng, (bounce + 1) | (delta << 31), __float_as_uint(geo.texcoord.x),
                             __float_as_uint(geo.texcoord.y)));
 #endif

@@ -11,3 +11,9 @@ timeout -k 10 300 python tools/shard_probe.py --onrun 1 --progressive 1 > gpurun
 cat gpurun_out/r04/shard_onrun.txt | cut -c1-200
 timeout -k 10 400 python bench.py > gpurun_out/r04/bench4_b.log 2>&1
 rc=$?; echo "bench4 rc=$rc"; grep '^{' gpurun_out/r04/bench4_b.log | tail -1 | cut -c1-400
+# kernel timeline of one rank's 1-spp OnRun cadence at N = 8 (where the fixed per-OnRun cost goes)
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r04/tl -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/shard_probe.py --onrun 1 --progressive 1 --worlds 8 --only-rank 0 --frames 3 > $GRAFT_REPO_ROOT/gpurun_out/r04/tl.log 2>&1
+rc=$?; echo "timeline rc=$rc"; cd $GRAFT_REPO_ROOT
+[ $rc -eq 0 ] && python3 tools/timeline.py gpurun_out/r04/tl/run_kernel_trace.csv 120 --list 40 > gpurun_out/r04/timeline_onrun8.txt && tail -20 gpurun_out/r04/timeline_onrun8.txt
+rm -f gpurun_out/r04/tl/run_kernel_trace.csv.gz

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--onrun", type=int, default=0,
                     help="1: the drop-in cadence -- a frame is 8 renders of 1 spp, each followed by a device "
                          "synchronisation (PTPass::OnRun, pt_pass.cpp:51-56), continuing one progressive render")
+    ap.add_argument("--only-rank", type=int, default=-1,
+                    help="render only this rank's share (a kernel trace of one rank's cadence)")
     args = ap.parse_args()
     import torch
 
@@ -43,7 +45,7 @@ def main():
     for n in args.worlds:
         per_rank = []
         host_ms = []
-        for r in range(n):
+        for r in (range(n) if args.only_rank < 0 else [args.only_rank]):
             pt.set_tiling(args.tile, r, n)
             pt.mark_dirty()
 
