@@ -180,6 +180,8 @@ def load_library(path: str | None = None):
         raise FileNotFoundError(f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = C.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
+        if p != LIB_PATH and not hasattr(lib, name):  # an older A/B build (PUPIL_LIB) lacks newer entry points
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -636,9 +636,11 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
                 nf.seed = pt->pipe.back().seed + fp.spp;
                 nf.aov_scratch = true;  // completes in a later render
             }
-            FrameParams fg = fp;
-            fg.seed0 = nf.seed;
-            launch_generate(pt->sc, fg, cx.view(nf.slot, np), s, !pt->fresh());
+            if (!(PUPIL_CAMGEN && pt->fresh())) {  // list shading generates the camera rays in the traversal
+                FrameParams fg = fp;
+                fg.seed0 = nf.seed;
+                launch_generate(pt->sc, fg, cx.view(nf.slot, np), s, !pt->fresh());
+            }
             started++;
         }
         if (had) {
@@ -657,17 +659,19 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
             }
             cx.ev0(1);
             cx.tail_slot();
+            const CameraGen cam{pt->fresh() ? 1u : 0u, nf.seed, fp.width, fp.height, fp.pixel_map};
             if (inject)  // + the new frame's camera rays, dequeued first in every chunk (pixel-major)
                 launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s, (uint32_t)np, 0u,
-                                   (uint32_t)(nf.slot * np), interleave, nl);
+                                   (uint32_t)(nf.slot * np), interleave, nl, &cam);
             else
                 launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s);
             cx.ev1();
         } else {
             cx.ev0(0);
             cx.tail_slot();
+            const CameraGen cam{pt->fresh() ? 1u : 0u, nf.seed, fp.width, fp.height, fp.pixel_map};
             launch_extend(pt->sc, cx.view(nf.slot, np), q, nullptr, nullptr, (uint32_t)np, pt->ovf, pt->ovf_threads,
-                          cx.tsp(), s, interleave, nl);
+                          cx.tsp(), s, interleave, nl, &cam);
             cx.ev1();
         }
         if (!pt->shade_list)  // material bins of every path traced in this iteration -> q.bins

@@ -30,6 +30,36 @@ namespace {
 
 using namespace tr;
 
+// __raygen__main's camera ray (main.cu:53-75): path p of a batch whose first frame has
+// seed seed0 (sample p / num_local, local pixel p % num_local); the RNG is initialised
+// from (pixel, seed) and the film jitter drawn x first.  Returns the RNG after the two
+// draws, the pixel, and the normalised world direction (the origin is the camera's).
+__device__ __forceinline__ uint32_t camera_path(const Camera &cam, uint32_t width, uint32_t height,
+                                                const uint32_t *pixel_map, uint32_t num_local, uint32_t seed0,
+                                                uint32_t p, uint32_t &pixel, vec3 &dir) {
+    const uint32_t s = p / num_local;
+    const uint32_t l = p - s * num_local;
+    pixel = pixel_map ? pixel_map[l] : l;
+    uint32_t rng = rng_init(pixel, seed0 + s);  // main.cu:53
+    const float jx = rng_next(rng);             // main.cu:55 (x drawn first)
+    const float jy = rng_next(rng);
+    const uint32_t y = pixel / width;
+    const uint32_t x = pixel - y * width;
+    const vec4 film = v4(((float)x + jx) / (float)width, ((float)y + jy) / (float)height, 0.f, 1.f);
+    const float *m = cam.s2c;
+    vec4 d = v4(dot(v4(m[0], m[1], m[2], m[3]), film), dot(v4(m[4], m[5], m[6], m[7]), film),
+                dot(v4(m[8], m[9], m[10], m[11]), film), dot(v4(m[12], m[13], m[14], m[15]), film));
+    const float inv_w = 1.0f / d.w;
+    d = v4(d.x * inv_w, d.y * inv_w, d.z * inv_w, d.w * inv_w);
+    d.w = 0.f;
+    d = normalize(d);
+    const float *c = cam.c2w;
+    dir = normalize(v3(dot(v4(c[0], c[1], c[2], c[3]), d), dot(v4(c[4], c[5], c[6], c[7]), d),
+                       dot(v4(c[8], c[9], c[10], c[11]), d)));
+    return rng;
+}
+__device__ __forceinline__ vec3 camera_origin(const Camera &cam) { return v3(cam.c2w[3], cam.c2w[7], cam.c2w[11]); }
+
 // Two-level: the object-space box ray of instance `in` (origin, reciprocal
 // direction) and its slab-test bound (pt_traverse.h slab_error_pad), which adds the
 // position margin at the exit of the instance's world box.
@@ -151,18 +181,37 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     float4 o, d;
                     if (MODE == kModeExtend) {
                         p = job.queue ? job.queue[i] : (job.spp ? (i % job.spp) * job.num_local + i / job.spp : i);
-                        o = ld_ps(ps.ray_o + p);
-                        d = ld_ps(ps.ray_d + p);
+                        if (PUPIL_CAMGEN && job.cam.on) {  // a camera ray, generated here (no k_generate pass)
+                            uint32_t pixel;
+                            vec3 dir;
+                            (void)camera_path(sc.camera, job.cam.width, job.cam.height, job.cam.pixel_map, job.num_local,
+                                              job.cam.seed0, p, pixel, dir);
+                            o = f4(camera_origin(sc.camera), 0.f);
+                            d = f4(dir, 0.f);
+                        } else {
+                            o = ld_ps(ps.ray_o + p);
+                            d = ld_ps(ps.ray_d + p);
+                        }
                         tmin = 0.001f;
                         tmax = kMaxDistance;
                     } else if (MODE == kModeMixedAhead && k < len_a) {
                         // a camera ray of the next render (generated into the other half of the
                         // path state): the primary extend's pixel-major dequeue, then the offset
                         const uint32_t j = lo_a + k;
-                        p = (job.spp ? (j % job.spp) * job.num_local + j / job.spp : j) + job.ahead_base;
+                        const uint32_t pl = job.spp ? (j % job.spp) * job.num_local + j / job.spp : j;
+                        p = pl + job.ahead_base;
                         any = false;
-                        o = ld_ps(ps.ray_o + p);
-                        d = ld_ps(ps.ray_d + p);
+                        if (PUPIL_CAMGEN && job.cam.on) {  // generated here (no k_generate pass)
+                            uint32_t pixel;
+                            vec3 dir;
+                            (void)camera_path(sc.camera, job.cam.width, job.cam.height, job.cam.pixel_map, job.num_local,
+                                              job.cam.seed0, pl, pixel, dir);
+                            o = f4(camera_origin(sc.camera), 0.f);
+                            d = f4(dir, 0.f);
+                        } else {
+                            o = ld_ps(ps.ray_o + p);
+                            d = ld_ps(ps.ray_d + p);
+                        }
                         tmin = 0.001f;
                         tmax = kMaxDistance;
                     } else if (kMixed) {
@@ -419,40 +468,23 @@ __device__ __forceinline__ uint32_t global_pixel(const FrameParams &fp, uint32_t
 
 // A fresh path's RNG after the camera ray's two draws (main.cu:53-55): path p of a batch whose
 // first frame has seed seed0 (sample p / num_local, local pixel p % num_local)
-__device__ __forceinline__ uint32_t camera_rng(const FrameParams &fp, uint32_t p, uint32_t seed0, float &jx,
-                                               float &jy, uint32_t &pixel) {
-    const uint32_t s = p / fp.num_local;
-    const uint32_t l = p - s * fp.num_local;
-    pixel = global_pixel(fp, l);
-    uint32_t rng = rng_init(pixel, seed0 + s);  // main.cu:53
-    jx = rng_next(rng);                         // main.cu:55 (x drawn first)
-    jy = rng_next(rng);
-    return rng;
+// a fresh path's RNG after the camera draws and its camera ray direction (camera_path)
+__device__ __forceinline__ uint32_t fresh_path(const DeviceScene &sc, const FrameParams &fp, uint32_t p, uint32_t seed0,
+                                               vec3 &dir) {
+    uint32_t pixel;
+    return camera_path(sc.camera, fp.width, fp.height, fp.pixel_map, fp.num_local, seed0, p, pixel, dir);
 }
 
 // full = 0 (list shading, PUPIL_FRESH_SHADE): only the camera ray is stored; the bounce-0
-// shade of the fresh paths takes throughput 1, radiance 0 and the RNG from camera_rng
-// instead of reading them (k_shade_all `fresh`)
+// shade of the fresh paths takes throughput 1, radiance 0 and the RNG from fresh_path
+// instead of reading them (k_shade_all `fresh`).  With in-kernel camera rays
+// (CameraGen) list renders need no generate pass at all.
 __global__ __launch_bounds__(kShadeBlock) void k_generate(DeviceScene sc, FrameParams fp, PathState ps, uint32_t full) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= fp.num_paths) return;
-    float jx, jy;
-    uint32_t pixel;
-    const uint32_t rng = camera_rng(fp, p, fp.seed0, jx, jy, pixel);
-    const uint32_t y = pixel / fp.width;
-    const uint32_t x = pixel - y * fp.width;
-    const vec4 film = v4(((float)x + jx) / (float)fp.width, ((float)y + jy) / (float)fp.height, 0.f, 1.f);
-    const float *m = sc.camera.s2c;
-    vec4 d = v4(dot(v4(m[0], m[1], m[2], m[3]), film), dot(v4(m[4], m[5], m[6], m[7]), film),
-                dot(v4(m[8], m[9], m[10], m[11]), film), dot(v4(m[12], m[13], m[14], m[15]), film));
-    const float inv_w = 1.0f / d.w;
-    d = v4(d.x * inv_w, d.y * inv_w, d.z * inv_w, d.w * inv_w);
-    d.w = 0.f;
-    d = normalize(d);
-    const float *c = sc.camera.c2w;
-    const vec3 dir = normalize(v3(dot(v4(c[0], c[1], c[2], c[3]), d), dot(v4(c[4], c[5], c[6], c[7]), d),
-                                  dot(v4(c[8], c[9], c[10], c[11]), d)));
-    st_ps(ps.ray_o + p, make_float4(c[3], c[7], c[11], 0.f));
+    vec3 dir;
+    const uint32_t rng = fresh_path(sc, fp, p, fp.seed0, dir);
+    st_ps(ps.ray_o + p, f4(camera_origin(sc.camera), 0.f));
     st_ps(ps.ray_d + p, make_float4(dir.x, dir.y, dir.z, 0.f));
     if (!full) return;
     st_ps(ps.thr + p, make_float4(1.f, 1.f, 1.f, 0.f));
@@ -472,8 +504,8 @@ struct HitGeo {
 // shading record (bvh_build.hip k_attrs: object-space vertices, normals, uvs).
 // ro_rec: the ray origin record, read only for a sphere hit (the triangle position is
 // interpolated from the vertices)
-__device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, const float4 *ro_rec, vec3 rd,
-                                             vec2 stale_uv) {
+__device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, const float4 *ro_rec, bool fresh,
+                                             vec3 rd, vec2 stale_uv) {
     HitGeo out;
     const uint32_t idx = __float_as_uint(h.w);
     // flat: idx = record in traversal order, which names the instance; two-level:
@@ -511,7 +543,7 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, c
     g.texcoord = stale_uv;
     uint32_t local = 0;
     if (sphere) {
-        const vec3 ro = f3(ld_ps(ro_rec));
+        const vec3 ro = PUPIL_CAMGEN && fresh ? camera_origin(sc.camera) : f3(ld_ps(ro_rec));
         g.position = ro + h.x * rd;
         const vec3 local_pos = xform_point(in.to_object, g.position);
         g.texcoord = sphere_texcoord(normalize(local_pos - v3(0.f)));
@@ -600,11 +632,18 @@ __device__ __forceinline__ bool last_sample(const FrameParams &fp, uint32_t p, u
 // RNG `fresh_rng`; k_generate stored only its camera ray)
 template <uint32_t MAT>
 __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
-                                              uint32_t p, bool fresh, uint32_t fresh_rng) {
+                                              uint32_t p, bool fresh, uint32_t fresh_p, uint32_t fresh_seed0) {
     bool push_next = false, push_shadow = false;
     const float4 h = ld_ps(ps.hit + p);
-    const float4 d4 = ld_ps(ps.ray_d + p);
-    const vec3 ray_d = f3(d4);
+    // a fresh path's camera ray and RNG are recomputed (the traversal generated the ray too)
+    vec3 ray_d;
+    uint32_t fresh_rng = 0;
+    if (PUPIL_CAMGEN && fresh) fresh_rng = fresh_path(sc, fp, fresh_p, fresh_seed0, ray_d);
+    else ray_d = f3(ld_ps(ps.ray_d + p));
+    if (!PUPIL_CAMGEN && fresh) {  // A/B: the stored camera ray, the RNG recomputed
+        vec3 unused;
+        fresh_rng = fresh_path(sc, fp, fresh_p, fresh_seed0, unused);
+    }
     const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ld_ps(ps.misc + p);
     uint32_t rng = misc.x;
     const uint32_t flags = misc.y;
@@ -617,7 +656,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     vec3 L_add = v3(0.f);
     const vec2 stale_uv = v2(__uint_as_float(misc.z), __uint_as_float(misc.w));
 
-    HitGeo hg = reconstruct(sc, h, ps.ray_o + p, ray_d, stale_uv);
+    HitGeo hg = reconstruct(sc, h, ps.ray_o + p, fresh, ray_d, stale_uv);
     const DevInstance &in = sc.instances[hg.inst];
     const DevMaterial &mat = sc.materials[in.material];
     if (mat.twosided && dot(-ray_d, hg.g.normal) < 0.f) hg.g.normal = -hg.g.normal;  // geometry.h:316-320
@@ -653,7 +692,8 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         const DevEmitter &e = sc.areas[hg.emitter];
         vec3 Le;
         float pdf_e;
-        emitter_eval_area(e, geo, f3(ld_ps(ps.ray_o + p)), Le, pdf_e);
+        emitter_eval_area(e, geo, PUPIL_CAMGEN && fresh ? camera_origin(sc.camera) : f3(ld_ps(ps.ray_o + p)), Le,
+                          pdf_e);
         if (!is_zero(pdf_e)) {
             const float mis = (flags >> 31) ? 1.f : mis_weight(prev_pdf, pdf_e * e.select_probability);
             L_add = T * Le * mis;
@@ -751,7 +791,10 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
 // Paths whose ray left the scene (__miss__default, main.cu:196-212, and the
 // env handling at main.cu:87-99 / 165-169).
 __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
-                                           uint32_t p, bool fresh, uint32_t fresh_rng) {
+                                           uint32_t p, bool fresh, uint32_t fresh_p, uint32_t fresh_seed0) {
+    vec3 fresh_d = v3(0.f);
+    uint32_t fresh_rng = 0;
+    if (fresh) fresh_rng = fresh_path(sc, fp, fresh_p, fresh_seed0, fresh_d);
     const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ld_ps(ps.misc + p);
     if ((misc.y & 0xFFFFFFu) == 0u) {
         float4 rad4 = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ld_ps(ps.rad + p);
@@ -760,7 +803,8 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
         if (sc.has_env) {
             vec3 Le;
             float pdf;
-            env_eval(*sc.env, f3(ld_ps(ps.ray_o + p)), f3(ld_ps(ps.ray_d + p)), Le, pdf);
+            if (PUPIL_CAMGEN && fresh) env_eval(*sc.env, camera_origin(sc.camera), fresh_d, Le, pdf);
+            else env_eval(*sc.env, f3(ld_ps(ps.ray_o + p)), f3(ld_ps(ps.ray_d + p)), Le, pdf);
             L = L + Le;  // main.cu:185, no MIS on the camera ray
         }
         const float test = rng_next(rng);
@@ -823,27 +867,22 @@ __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))
         // the range part of a list launch is a fresh frame; with fresh_range its paths'
         // throughput, radiance and RNG were never stored (k_generate full = 0)
         const bool fresh = LIST != kShadeBins && fresh_range && i >= n_list;
-        uint32_t fresh_rng = 0;
-        if (fresh) {
-            float jx, jy;
-            uint32_t pixel;
-            fresh_rng = camera_rng(fp, p - range_base, fresh_seed0, jx, jy, pixel);
-        }
+        const uint32_t fresh_p = p - range_base;
         uint32_t flags = 0;
         switch (bin) {
-        case 0: shade_miss(sc, fp, ps, p, fresh, fresh_rng); break;
-        case PUPIL_MAT_DIFFUSE: flags = shade_hit<PUPIL_MAT_DIFFUSE>(sc, fp, ps, p, fresh, fresh_rng); break;
-        case PUPIL_MAT_DIELECTRIC: flags = shade_hit<PUPIL_MAT_DIELECTRIC>(sc, fp, ps, p, fresh, fresh_rng); break;
+        case 0: shade_miss(sc, fp, ps, p, fresh, fresh_p, fresh_seed0); break;
+        case PUPIL_MAT_DIFFUSE: flags = shade_hit<PUPIL_MAT_DIFFUSE>(sc, fp, ps, p, fresh, fresh_p, fresh_seed0); break;
+        case PUPIL_MAT_DIELECTRIC: flags = shade_hit<PUPIL_MAT_DIELECTRIC>(sc, fp, ps, p, fresh, fresh_p, fresh_seed0); break;
         case PUPIL_MAT_ROUGH_DIELECTRIC:
-            flags = shade_hit<PUPIL_MAT_ROUGH_DIELECTRIC>(sc, fp, ps, p, fresh, fresh_rng);
+            flags = shade_hit<PUPIL_MAT_ROUGH_DIELECTRIC>(sc, fp, ps, p, fresh, fresh_p, fresh_seed0);
             break;
-        case PUPIL_MAT_CONDUCTOR: flags = shade_hit<PUPIL_MAT_CONDUCTOR>(sc, fp, ps, p, fresh, fresh_rng); break;
+        case PUPIL_MAT_CONDUCTOR: flags = shade_hit<PUPIL_MAT_CONDUCTOR>(sc, fp, ps, p, fresh, fresh_p, fresh_seed0); break;
         case PUPIL_MAT_ROUGH_CONDUCTOR:
-            flags = shade_hit<PUPIL_MAT_ROUGH_CONDUCTOR>(sc, fp, ps, p, fresh, fresh_rng);
+            flags = shade_hit<PUPIL_MAT_ROUGH_CONDUCTOR>(sc, fp, ps, p, fresh, fresh_p, fresh_seed0);
             break;
-        case PUPIL_MAT_PLASTIC: flags = shade_hit<PUPIL_MAT_PLASTIC>(sc, fp, ps, p, fresh, fresh_rng); break;
-        case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p, fresh, fresh_rng); break;
-        default: flags = shade_hit<0u>(sc, fp, ps, p, fresh, fresh_rng); break;
+        case PUPIL_MAT_PLASTIC: flags = shade_hit<PUPIL_MAT_PLASTIC>(sc, fp, ps, p, fresh, fresh_p, fresh_seed0); break;
+        case PUPIL_MAT_ROUGH_PLASTIC: flags = shade_hit<PUPIL_MAT_ROUGH_PLASTIC>(sc, fp, ps, p, fresh, fresh_p, fresh_seed0); break;
+        default: flags = shade_hit<0u>(sc, fp, ps, p, fresh, fresh_p, fresh_seed0); break;
         }
         if (fp.nee_count) {  // collect_stats only: the reference's shadow-ray count, one atomic per wave
             const unsigned long long m = __ballot((flags & 4u) != 0u);
@@ -974,18 +1013,21 @@ void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathSta
 
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
                    const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
-                   const TraceStats *stats, hipStream_t s, uint32_t interleave_spp, uint32_t num_local) {
-    const TraceJob job{queue,   queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min,
-                       nullptr, nullptr,     queue ? 0u : interleave_spp, num_local};
+                   const TraceStats *stats, hipStream_t s, uint32_t interleave_spp, uint32_t num_local,
+                   const CameraGen *cam) {
+    TraceJob job{queue,   queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min,
+                 nullptr, nullptr,     queue ? 0u : interleave_spp, num_local};
+    if (cam && !queue) job.cam = *cam;
     launch_trace4<kModeExtend, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
 }
 
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                         const TraceStats *stats, hipStream_t s, uint32_t ahead_count, uint32_t list_base,
-                        uint32_t ahead_base, uint32_t ahead_spp, uint32_t ahead_local) {
-    const TraceJob job{nullptr,       nullptr,   ahead_count,          q.work + kWorkExtend,
-                       sc.trace_refill, sc.trace_node_min, nullptr, nullptr,
-                       ahead_count ? ahead_spp : 0u, ahead_local, list_base, ahead_base};
+                        uint32_t ahead_base, uint32_t ahead_spp, uint32_t ahead_local, const CameraGen *cam) {
+    TraceJob job{nullptr,       nullptr,   ahead_count,          q.work + kWorkExtend,
+                 sc.trace_refill, sc.trace_node_min, nullptr, nullptr,
+                 ahead_count ? ahead_spp : 0u, ahead_local, list_base, ahead_base};
+    if (cam && ahead_count) job.cam = *cam;
     if (ahead_count) launch_trace4<kModeMixedAhead, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
     else launch_trace4<kModeMixed, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
 }
