@@ -945,6 +945,8 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     }
     if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
     if (const char *g = std::getenv("PUPIL_PIPE_PATHS")) pt->pipe_paths = std::max(1.0, std::atof(g));
+    // PUPIL_TRAVERSAL=fused: the if-if kernel (trace4_body FUSED) for the flat / world-mode BVH4
+    if (const char *tv = std::getenv("PUPIL_TRAVERSAL")) sc.trace_fused = std::strcmp(tv, "fused") == 0 ? 1u : 0u;
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     if (nodes4_count(pt) > kMaxNodes4)

@@ -86,7 +86,14 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
 // instance each; entering one pushes the pending TLAS link and kReturnLink and
 // switches the box tests to the instance's object-space ray; popping
 // kReturnLink switches back.  Spheres are tested at their TLAS leaf.
-template <int MODE, bool ANY, bool STATS, bool TL>
+// FUSED (flat / world-mode nodes only, not TL): one work item per lane per iteration --
+// a node visit or one primitive record of the leaf the lane is in, both fetched as the
+// same 16-dword load -- instead of the while-while node and leaf phases.  The kernel is
+// latency bound (the waves of a SIMD mostly wait on their fetches), so every lane's next
+// item rides on each memory round trip: a lane that reaches a leaf no longer idles until
+// the wave leaves the node phase, nor the node lanes during the leaf phase.  Hits are
+// resolved by the (t, id) order, so the closest hit does not depend on the visit order.
+template <int MODE, bool ANY, bool STATS, bool TL, bool FUSED = false>
 __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathState &ps, const Queues &q,
                                             const TraceJob &job, int *ovf, uint32_t ovf_threads,
                                             const TraceStats &stats, int *s_ring) {
@@ -125,6 +132,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     RayPre r{};
     float tmin = MODE == kModeRays ? 0.f : 0.001f, tmax = 0.f, b1 = 0.f, b2 = 0.f;  // tmin: a constant outside kModeRays
     int node = kSentinel, leaf = 0;
+    uint32_t rec = 0, rec_end = 0;  // FUSED: the records [rec, rec_end) of the leaf being tested
     bool found = false;
     bool any = ANY;  // this lane's ray terminates on its first hit
     bool in_blas = false;  // TL: traversing an instance's BLAS
@@ -247,6 +255,11 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         leaf = node;
                         node = kSentinel;
                     }
+                    if (FUSED) {  // the whole scene is one leaf: test it first
+                        rec = leaf < 0 ? leaf_first(leaf) : 0u;
+                        rec_end = leaf < 0 ? rec + leaf_count(leaf) : 0u;
+                        leaf = 0;
+                    }
                     active = true;
                 }
             }
@@ -256,8 +269,86 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             if (drained) break;
             continue;
         }
+        // ---- FUSED: one node visit or one record test per lane
+        if (FUSED && active && !(any && found)) {
+            const bool in_leaf = rec < rec_end;
+            const float4 *src = in_leaf ? sc.prims + 3 * (size_t)rec
+                                        : reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(sc.nodes4) +
+                                                                            ((uint32_t)node << 6));
+            const float4 q0 = src[0], q1 = src[1], q2 = src[2];
+            float4 q3 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!in_leaf) q3 = src[3];
+            // the next link of the lane: a leaf link opens its record range, else the node
+            auto take = [&](int link) {
+                if (link < 0) {
+                    rec = leaf_first(link);
+                    rec_end = rec + leaf_count(link);
+                    node = kSentinel;
+                } else {
+                    node = link;
+                }
+            };
+            if (in_leaf) {
+                uint32_t &np_cnt = kMixed && any ? npt_sh : npt;
+                if (STATS) np_cnt++;
+                const uint32_t ref = __float_as_uint(q0.w);
+                const uint32_t key = ref & ~kPrimSphereBit;
+                float t, h1 = 0.f, h2 = 0.f;
+                bool hit;
+                if (ref & kPrimSphereBit) {
+                    const DevInstance &in = sc.instances[__float_as_uint(q1.w)];
+                    hit = intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, t);
+                } else {
+                    hit = intersect_triangle(r, v3(q0.x, q0.y, q0.z), v3(q1.x, q1.y, q1.z), v3(q2.x, q2.y, q2.z), tmin,
+                                             tmax, t, h1, h2);
+                }
+                if (hit && (any || t < tmax || key < best_key)) {
+                    tmax = t;
+                    best_key = key;
+                    best_idx = rec;
+                    b1 = h1;
+                    b2 = h2;
+                    found = true;
+                }
+                rec++;
+                if (rec == rec_end && !(any && found)) take(st.pop());
+            } else {
+                Bvh4Node n;
+                __builtin_memcpy(reinterpret_cast<char *>(&n), &q0, 16);
+                __builtin_memcpy(reinterpret_cast<char *>(&n) + 16, &q1, 16);
+                __builtin_memcpy(reinterpret_cast<char *>(&n) + 32, &q2, 16);
+                __builtin_memcpy(reinterpret_cast<char *>(&n) + 48, &q3, 16);
+                if (STATS) {
+                    if (kMixed && any) nv_sh++;
+                    else nv++;
+                    const unsigned long long m = __ballot(true);
+                    if ((int)lane_id() == __ffsll((long long)m) - 1) {
+                        dg[0]++;
+                        dg[1] += (unsigned long long)__popcll(m);
+                    }
+                    bool dup = false;
+                    for (int j = 0; j < 64; j++) {
+                        const int nj = __shfl(node, j);
+                        if (j < (int)lane_id() && ((m >> j) & 1ull) && nj == node) dup = true;
+                    }
+                    n_unique += dup ? 0u : 1u;
+                }
+                float t[4];
+                int l[4];
+                visit4(n, r.o, r.idir, be, tmin, tmax, t, l);
+                if (t[0] == kInf) {
+                    take(st.pop());
+                } else {
+                    st.reserve3();
+                    st.push(l[3], t[3] != kInf);
+                    st.push(l[2], t[2] != kInf);
+                    st.push(l[1], t[1] != kInf);
+                    take(l[0]);
+                }
+            }
+        }
         // ---- traverse until this lane's ray terminates or it needs a leaf while others do too
-        if (active) {
+        if (!FUSED && active) {
             while ((uint32_t)node < (uint32_t)kSentinel) {
                 const Bvh4Node n = load_node4(sc, node);
                 if (STATS) {
@@ -362,7 +453,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 }
             }
         }
-        const bool done = active && ((node == kSentinel && leaf >= 0) || (any && found));
+        const bool done = active && ((node == kSentinel && leaf >= 0 && rec >= rec_end) || (any && found));
         // ---- retire
         if (MODE == kModeExtend || kMixed) {
             uint32_t bin = 0;
@@ -449,6 +540,14 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
     __shared__ int s_ring[kRing * kTraceBlock];
     trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring);
+}
+
+// fused node / record steps (trace4_body FUSED; PUPIL_TRAVERSAL=fused)
+template <int MODE, bool ANY, bool STATS>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4f(
+    DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
+    __shared__ int s_ring[kRing * kTraceBlock];
+    trace4_body<MODE, ANY, STATS, false, true>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring);
 }
 
 // two-level variant: 9 more live registers (object-space box ray, margin,
@@ -966,6 +1065,13 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
                                ovf, ovf_threads, st);
         else
             hipLaunchKernelGGL((k_trace4tl<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                               ovf, ovf_threads, st);
+    } else if (sc.trace_fused) {
+        if (stats)
+            hipLaunchKernelGGL((k_trace4f<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                               ovf, ovf_threads, st);
+        else
+            hipLaunchKernelGGL((k_trace4f<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
                                ovf, ovf_threads, st);
     } else if (stats) {
         hipLaunchKernelGGL((k_trace4<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
