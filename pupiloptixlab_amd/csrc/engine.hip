@@ -112,14 +112,20 @@ struct pupil_pt {
     // are dropped on any change.  ahead_mode: 1 = single-spp renders or the hint,
     // 2 = every render, 0 = off (PUPIL_AHEAD).
     int ahead_mode = 1;
+    // a group of `frames` consecutive frames (seeds seed, seed + spp, ...) in one ring slot
     struct PipeFrame {
         uint32_t slot, seed, phases;  // phases = bounces traced + shaded so far (complete at max_depth)
-        bool aov_scratch;             // shaded ahead of its render: AOVs wait in the slot's scratch
+        bool aov_scratch;             // AOVs wait in the slot's scratch until each frame's render
+        uint32_t frames, consumed;    // frames in the group; accumulated (rendered) so far
     };
     std::vector<PipeFrame> pipe;      // in flight, oldest first
     uint32_t pipe_slots = 0;          // K of the ring in use
     size_t pipe_np = 0;               // paths per slot
-    uint32_t pipe_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // w, h, tile size, rank, world, spp, depth, local pixels
+    uint32_t pipe_key[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // w, h, tile size, rank, world, spp, depth, local pixels, G
+    size_t pipe_cap = 0;              // paths per ring slot (G frames)
+    // PUPIL_PIPE_GROUP_PATHS: renders of fewer paths batch G = ceil(this / paths) frames per slot
+    double pipe_group_paths = 8e6;
+    bool ring_fresh = true;           // the ring was (re)allocated: its flags bytes are not yet cleared
     uint32_t pipe_run = 0;            // consecutive renders that continued the previous one
     uint32_t pipe_next_seed = 0;      // random_seed of the render that would continue the last one
     uint32_t pipe_gen = 0;            // iterations so far (flags tags)
@@ -220,6 +226,7 @@ struct pupil_pt {
     }
     void release_state() {
         ring_bytes = 0;
+        ring_fresh = true;
         void *bufs[] = {ps.ray_o, ps.ray_d, ps.hit,  ps.thr,  ps.rad,    ps.misc,
                         ps.sh_d, ps.sh_c, ps.mbin, ps.sflags, q.bins, q.nxsh, q.hist};
         for (void *b : bufs)
@@ -527,9 +534,9 @@ struct RenderCtx {
             ts_dev.wave_times = nullptr;
     }
     // path state of ring slot h: every array offset by h * paths
-    PathState view(uint32_t h, size_t paths) const {
+    PathState view(uint32_t h, size_t paths, size_t extra = 0) const {
         PathState v = pt->ps;
-        const size_t o = (size_t)h * paths;
+        const size_t o = (size_t)h * paths + extra;
         v.ray_o += o, v.ray_d += o, v.hit += o, v.thr += o, v.rad += o, v.misc += o;
         v.sh_d += o, v.sh_c += o, v.mbin += o, v.sflags += o;
         return v;
@@ -563,91 +570,128 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
     const bool may_pipe = pt->ahead_mode != 0 &&
                           (pt->ahead_mode == 2 || launch->spp == 1 || (launch->hints & PUPIL_HINT_CONTINUE)) && !cx.stats &&
                           D >= 2 && D <= 63;  // the 6-bit flags tags of a slot stay unambiguous for 63 iterations
-    uint32_t K = 1;
+    // frames ahead are started only once a continuation is likely: the caller said so
+    // (PUPIL_HINT_CONTINUE), or the last render was continued too.  A render after a change
+    // (a camera moving every OnRun) then traces nothing it may discard.
+    const bool cont_seed = pt->pipe_valid && pt->pipe_next_seed == launch->random_seed;
+    const bool speculate = (launch->hints & PUPIL_HINT_CONTINUE) || pt->ahead_mode == 2 ||
+                           (cont_seed && pt->pipe_run >= 1);
+    uint32_t K = 1, G = 1;
     if (may_pipe) {
+        // frame groups: renders smaller than PUPIL_PIPE_GROUP_PATHS (one rank's tiles at the
+        // 1-spp OnRun cadence) batch G consecutive frames per ring slot, so each traversal
+        // launch carries enough rays to amortise its tail; the renders whose frame an earlier
+        // render already completed only accumulate it
+        G = (uint32_t)std::min(64.0, std::max(1.0, std::ceil(pt->pipe_group_paths / (double)np)));
         K = pt->pipe_limit ? std::min(pt->pipe_limit, D) : D;
         constexpr double kPathBytes = 8 * 16 + 2 + 4 + 8 + 1;  // PathState + bins + nxsh + partition scratch
-        K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::floor(pt->pipe_budget / ((double)np * kPathBytes))));
-        K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::ceil(pt->pipe_paths / (double)np)));
-        while (K > 1 && (uint64_t)K * np >= (1ull << 31)) K--;
+        K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::floor(pt->pipe_budget / ((double)G * np * kPathBytes))));
+        K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::ceil(pt->pipe_paths / ((double)G * np))));
+        while (K * G > 1 && (uint64_t)K * G * np >= (1ull << 31)) {
+            if (G > 1) G--;
+            else K--;
+        }
     }
-    const uint32_t key[8] = {cx.key[0], cx.key[1], cx.key[2], cx.key[3], cx.key[4], fp.spp, D, fp.num_local};
+    uint32_t key[9] = {cx.key[0], cx.key[1], cx.key[2], cx.key[3], cx.key[4], fp.spp, D, fp.num_local, G};
     // this render continues the last one (OnRun cadence: the next seed, nothing changed);
     // frames in flight, if any, are then exactly the ones it and its successors need
-    bool reset = !(pt->pipe_valid && K == pt->pipe_slots && np == pt->pipe_np &&
-                   std::memcmp(key, pt->pipe_key, sizeof(key)) == 0 && pt->pipe_next_seed == launch->random_seed &&
-                   (pt->pipe.empty() || pt->pipe.front().seed == launch->random_seed));
-    if ((size_t)K * np > pt->cap) {  // growing the ring loses its contents
+    bool reset = !(cont_seed && K == pt->pipe_slots && np == pt->pipe_np &&
+                   std::memcmp(key, pt->pipe_key, sizeof(key)) == 0 &&
+                   (pt->pipe.empty() ||
+                    pt->pipe.front().seed + pt->pipe.front().consumed * fp.spp == launch->random_seed));
+    const uint32_t nl = fp.num_local;
+    if ((size_t)K * G * np > pt->cap) {  // growing the ring loses its contents
         reset = true;
-        int rc = ensure_state(pt, (size_t)K * np);
-        while (rc == PUPIL_ERR_OOM && K > 1) {  // a smaller ring, down to no frames ahead
-            K = K > 2 ? K / 2 : 1;
-            rc = ensure_state(pt, (size_t)K * np);
+        pt->pipe.clear();
+        int rc = ensure_state(pt, (size_t)K * G * np);
+        while (rc == PUPIL_ERR_OOM && K * G > 1) {  // a smaller ring, down to no frames ahead
+            if (K > 1) K = K > 2 ? K / 2 : 1;
+            else G = G > 2 ? G / 2 : 1;
+            rc = ensure_state(pt, (size_t)K * G * np);
         }
         if (rc) return rc;
+        key[8] = G;
     }
-    const uint32_t nl = fp.num_local;
-    if (K > 1 && (size_t)K * 7 * nl > pt->aov_cap) {
+    const size_t cap_paths = (size_t)G * np;  // paths per ring slot
+    if (K * G > 1 && (size_t)K * G * 7 * nl > pt->aov_cap) {
         reset = true;
         if (pt->aov_scratch) (void)hipFree(pt->aov_scratch);
         pt->aov_scratch = nullptr;
         pt->aov_cap = 0;
-        HIP_TRY(hipMalloc((void **)&pt->aov_scratch, sizeof(float) * (size_t)K * 7 * nl));
-        pt->aov_cap = (size_t)K * 7 * nl;
+        HIP_TRY(hipMalloc((void **)&pt->aov_scratch, sizeof(float) * (size_t)K * G * 7 * nl));
+        pt->aov_cap = (size_t)K * G * 7 * nl;
     }
     const PathState ring = pt->ps;
     if (reset) {
+        // the dropped frames' flags / bins bytes are cleared (every other byte of the ring is
+        // clear: a completed frame's accumulate clears its own)
+        for (const auto &g : pt->pipe) {
+            const size_t off = (size_t)g.slot * pt->pipe_cap, len = (size_t)g.frames * pt->pipe_np;
+            if (off + len > pt->cap) continue;
+            HIP_TRY(hipMemsetAsync(ring.sflags + off, 0, len, s));
+            if (!pt->shade_list) HIP_TRY(hipMemsetAsync(ring.mbin + off, 0xFF, len, s));
+        }
+        if (pt->ring_fresh) {  // a new allocation: everything
+            HIP_TRY(hipMemsetAsync(ring.sflags, 0, pt->cap, s));
+            if (!pt->shade_list) HIP_TRY(hipMemsetAsync(ring.mbin, 0xFF, pt->cap, s));
+            pt->ring_fresh = false;
+        }
         pt->pipe.clear();
         pt->pipe_run = 0;
         pt->pipe_slots = K;
         pt->pipe_np = np;
+        pt->pipe_cap = cap_paths;
         std::memcpy(pt->pipe_key, key, sizeof(key));
-        if (K > 1) {  // no stale flags / bins in slots this render does not start
-            HIP_TRY(hipMemsetAsync(ring.sflags, 0, (size_t)K * np, s));
-            if (!pt->shade_list) HIP_TRY(hipMemsetAsync(ring.mbin, 0xFF, (size_t)K * np, s));
-        }
     } else {
         pt->pipe_run++;
     }
     pt->pipe_valid = true;
     Queues &q = pt->q;
-    const uint32_t nring = (uint32_t)((size_t)K * np);
-    const uint32_t interleave = pt->primary_interleave && fp.spp > 1 ? fp.spp : 0u;
+    // the flags partition scans the slots in use: [0, end of the last frame group)
+    auto ring_end = [&]() {
+        size_t e = 0;
+        for (const auto &g : pt->pipe) e = std::max(e, (size_t)g.slot * cap_paths + (size_t)g.frames * np);
+        return (uint32_t)e;
+    };
+    const uint32_t interleave0 = pt->primary_interleave;
+    // iterations this render needs: none when an earlier render completed its frame
     const uint32_t L = pt->pipe.empty() ? D : D - pt->pipe.front().phases;
-    auto scratch = [&](uint32_t slot) { return pt->aov_scratch + (size_t)slot * 7 * nl; };
+    // AOV scratch of ring slot `slot`, frame `f` of its group: 7 floats per local pixel
+    auto scratch = [&](uint32_t slot, uint32_t f) { return pt->aov_scratch + ((size_t)slot * G + f) * 7 * nl; };
     uint64_t started = 0;
-    // frames ahead are started only once a continuation is likely: the caller said so
-    // (PUPIL_HINT_CONTINUE), or this render already continued the previous one.  A render
-    // after a change (a camera moving every OnRun) then traces nothing it may discard.
-    const bool speculate = (launch->hints & PUPIL_HINT_CONTINUE) || pt->pipe_run >= 1 || pt->ahead_mode == 2;
     // depths above 64: every 16 iterations the host reads the list lengths back and stops
     // once no path is left (all of them missed, were absorbed or were terminated by RR)
     const bool deep_exit = D > 64 && K == 1;
     pt->snap_taken = false;
     for (uint32_t it = 0; it < L; it++) {
         const bool had = !pt->pipe.empty();
-        // start a frame: this render's own on an empty pipeline, else the next one ahead
-        // in the last run + 1 iterations while a slot is free
+        // start a frame group: this render's own on an empty pipeline (one frame unless
+        // speculating), else the next one ahead in the last run + 1 iterations while a slot is free
         const bool inject = !had || (speculate && pt->pipe.size() < K && it + pt->pipe_run + 1 >= L);
-        pupil_pt::PipeFrame nf{0u, launch->random_seed, 0u, false};
+        pupil_pt::PipeFrame nf{0u, launch->random_seed, 0u, false, speculate ? G : 1u, 0u};
+        if (inject && had) {
+            nf.slot = (pt->pipe.back().slot + 1) % K;
+            nf.seed = pt->pipe.back().seed + pt->pipe.back().frames * fp.spp;
+        }
+        nf.aov_scratch = had || nf.frames > 1;  // AOVs wait in the slot's scratch until the frame's render
+        const uint32_t nfp = (uint32_t)(nf.frames * np);  // paths of the new group
+        const uint32_t gspp = nf.frames * fp.spp;         // its samples per pixel
+        const uint32_t interleave = interleave0 && gspp > 1 ? gspp : 0u;
         if (inject) {
-            if (had) {
-                nf.slot = (pt->pipe.back().slot + 1) % K;
-                nf.seed = pt->pipe.back().seed + fp.spp;
-                nf.aov_scratch = true;  // completes in a later render
-            }
             if (!(PUPIL_CAMGEN && pt->fresh())) {  // list shading generates the camera rays in the traversal
                 FrameParams fg = fp;
                 fg.seed0 = nf.seed;
-                launch_generate(pt->sc, fg, cx.view(nf.slot, np), s, !pt->fresh());
+                fg.num_paths = nfp;
+                launch_generate(pt->sc, fg, cx.view(nf.slot, cap_paths), s, !pt->fresh());
             }
-            started++;
+            started += nfp;
         }
+        const CameraGen cam{pt->fresh() ? 1u : 0u, nf.seed, fp.width, fp.height, fp.pixel_map};
         if (had) {
-            // the rays the previous iteration's shade spawned, over the whole ring, in
+            // the rays the previous iteration's shade spawned, over the slots in use, in
             // increasing path id: next (bit 0) and shadow (bit 1) lists -> q.nxsh
             const uint32_t tag = pt->pipe_gen % 63u + 1u;
-            launch_partition(ring.sflags, nring, 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
+            launch_partition(ring.sflags, ring_end(), 2, kPartFlags, tag, q.nxsh, q.hist, q.counts + kCntNext,
                              q.counts + kStartNext, nullptr, nullptr, s, pt->ray_cum,
                              pt->snap_taken ? nullptr : pt->ray_cum + 2);
             pt->snap_taken = true;
@@ -659,55 +703,61 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
             }
             cx.ev0(1);
             cx.tail_slot();
-            const CameraGen cam{pt->fresh() ? 1u : 0u, nf.seed, fp.width, fp.height, fp.pixel_map};
-            if (inject)  // + the new frame's camera rays, dequeued first in every chunk (pixel-major)
-                launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s, (uint32_t)np, 0u,
-                                   (uint32_t)(nf.slot * np), interleave, nl, &cam);
+            if (inject)  // + the new group's camera rays, dequeued first in every chunk (pixel-major)
+                launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s, nfp, 0u,
+                                   (uint32_t)(nf.slot * cap_paths), interleave, nl, &cam);
             else
                 launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s);
             cx.ev1();
         } else {
             cx.ev0(0);
             cx.tail_slot();
-            const CameraGen cam{pt->fresh() ? 1u : 0u, nf.seed, fp.width, fp.height, fp.pixel_map};
-            launch_extend(pt->sc, cx.view(nf.slot, np), q, nullptr, nullptr, (uint32_t)np, pt->ovf, pt->ovf_threads,
+            launch_extend(pt->sc, cx.view(nf.slot, cap_paths), q, nullptr, nullptr, nfp, pt->ovf, pt->ovf_threads,
                           cx.tsp(), s, interleave, nl, &cam);
             cx.ev1();
         }
+        if (inject) {  // the group is in flight from here (ring_end covers it)
+            nf.phases = 0;
+            pt->pipe.push_back(nf);
+        }
+        const uint32_t nring = ring_end();
         if (!pt->shade_list)  // material bins of every path traced in this iteration -> q.bins
             launch_partition(ring.mbin, nring, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
                              q.counts + kStartBins, q.counts + kScratch, nullptr, s);
         FrameParams fs = fp;
-        if (inject && nf.aov_scratch) {  // AOVs of a frame ahead wait in its slot's scratch
-            fs.albedo = scratch(nf.slot);
+        fs.group = G;  // AOV frame of a sample: its group frame (samples per ring slot = G spp)
+        if (inject && nf.aov_scratch) {  // AOVs of frames ahead wait in their slot's scratch
+            fs.albedo = scratch(nf.slot, 0);
             fs.normal = fs.albedo + 3 * (size_t)nl;
             fs.test = fs.albedo + 6 * (size_t)nl;
             fs.aov_local = 1;
+            fs.aov_frame_stride = (uint32_t)(7 * nl);
         }
         if (D > 63) HIP_TRY(hipMemsetAsync(ring.sflags, 0, nring, s));  // K = 1: tags would alias
         const uint32_t wtag = (pt->pipe_gen + 1u) % 63u + 1u;
         const ShadeList list = !pt->shade_list ? kShadeBins : (had ? (inject ? kShadeNextRange : kShadeNext) : kShadeAll);
-        const uint32_t max_count = (uint32_t)std::min<uint64_t>(
-            nring, (had ? (uint64_t)pt->pipe.size() * np : 0u) + (inject ? np : 0u));
+        uint64_t live = 0;  // paths the launch may list
+        for (const auto &g : pt->pipe) live += (uint64_t)g.frames * np;
+        const uint32_t max_count = (uint32_t)std::min<uint64_t>(nring, live);
         cx.ev0(2);
-        launch_shade(pt->sc, fs, ring, q, wtag, s, list, (uint32_t)(nf.slot * np), inject ? (uint32_t)np : 0u, max_count,
+        launch_shade(pt->sc, fs, ring, q, wtag, s, list, (uint32_t)(nf.slot * cap_paths), inject ? nfp : 0u, max_count,
                      pt->fresh(), nf.seed);
         cx.ev1();
         pt->pipe_gen++;
         for (auto &f : pt->pipe) f.phases++;
-        if (inject) {
-            nf.phases = 1;
-            pt->pipe.push_back(nf);
-        }
     }
-    // this render's frame is complete: accumulate it and free its slot
-    const pupil_pt::PipeFrame f = pt->pipe.front();
-    pt->pipe.erase(pt->pipe.begin());
-    launch_accumulate(fp, cx.view(f.slot, np), f.aov_scratch ? scratch(f.slot) : nullptr, K > 1, s);
+    // this render's frame is complete: accumulate it; the group's slot is free once all
+    // its frames are accumulated
+    pupil_pt::PipeFrame &g = pt->pipe.front();
+    const uint32_t f = g.consumed;
+    // (the accumulate clears the frame's flags bytes: no stale tag is ever listed again)
+    launch_accumulate(fp, cx.view(g.slot, cap_paths, (size_t)f * np), g.aov_scratch ? scratch(g.slot, f) : nullptr,
+                      true, s);
+    if (++g.consumed == g.frames) pt->pipe.erase(pt->pipe.begin());
     pt->pipe_next_seed = launch->random_seed + fp.spp;
     pt->last_iters = L;
-    pt->last_primary = started * np;
-    pt->primary_cum += started * np;
+    pt->last_primary = started;
+    pt->primary_cum += started;
     return PUPIL_OK;
 }
 
@@ -945,6 +995,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     }
     if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
     if (const char *g = std::getenv("PUPIL_PIPE_PATHS")) pt->pipe_paths = std::max(1.0, std::atof(g));
+    if (const char *g = std::getenv("PUPIL_PIPE_GROUP_PATHS")) pt->pipe_group_paths = std::max(1.0, std::atof(g));
     // PUPIL_TRAVERSAL=fused: the if-if kernel (trace4_body FUSED) for the flat / world-mode BVH4
     if (const char *tv = std::getenv("PUPIL_TRAVERSAL")) sc.trace_fused = std::strcmp(tv, "fused") == 0 ? 1u : 0u;
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
@@ -1249,7 +1300,8 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
     unsigned long long cum[4] = {0, 0, 0, 0};  // running totals, then their values before the last render
     HIP_TRY(hipMemcpy(cum, pt->ray_cum, sizeof(cum), hipMemcpyDeviceToHost));
     c.rays_traced_total = pt->primary_cum + cum[0] + cum[1];
-    c.frames_in_flight = pt->pipe.size();
+    c.frames_in_flight = 0;  // frames started ahead of the next render (in groups: not yet accumulated)
+    for (const auto &g : pt->pipe) c.frames_in_flight += g.frames - g.consumed;
     c.pipeline_slots = pt->pipe_slots;
     c.tlas_sah_splits = pt->two_level ? pt->tl.sah_splits : 0u;
     c.ring_bytes = pt->ring_bytes + sizeof(float) * (uint64_t)pt->aov_cap;

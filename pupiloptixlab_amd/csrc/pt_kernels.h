@@ -103,6 +103,11 @@ struct FrameParams {
     // shade: the AOV pointers above are indexed by the local pixel (compact output, or the
     // per-slot AOV scratch of a frame that completes in a later render); else by y*w+x
     uint32_t aov_local;
+    // pipelined frame groups (engine.hip render_pipelined): a ring slot holds `group` frames of
+    // spp samples; frame f of a slot writes its AOVs at + f * aov_frame_stride floats (0: one
+    // frame per slot, or the render's own buffers)
+    uint32_t group;
+    uint32_t aov_frame_stride;
 };
 
 // Path-state records are streamed with non-temporal loads / stores (PUPIL_NT, A/B builds: 0),

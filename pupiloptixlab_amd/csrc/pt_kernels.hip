@@ -720,10 +720,13 @@ __device__ __forceinline__ const DevEmitter *select_emitter(const DeviceScene &s
 // its bounce is PathState::misc.y (loaded inside shade_hit / shade_miss: passing the
 // record in from the launch kept it live across the whole shade, 137 instead of 123
 // VGPRs, one wave less per SIMD).
-// Last sample of its frame, and the local pixel (AOVs are written for the last sample).
-__device__ __forceinline__ bool last_sample(const FrameParams &fp, uint32_t p, uint32_t &l) {
+// Last sample of its frame, and the local pixel (AOVs are written for the last sample);
+// `frame_off`: the AOV offset of the sample's frame within a ring slot's frame group.
+__device__ __forceinline__ bool last_sample(const FrameParams &fp, uint32_t p, uint32_t &l, size_t &frame_off) {
     const uint32_t q = p / fp.num_local;
     l = p - q * fp.num_local;
+    const uint32_t g = fp.group > 1u ? fp.group : 1u;
+    frame_off = (size_t)((q % (g * fp.spp)) / fp.spp) * fp.aov_frame_stride;
     return q % fp.spp + 1u == fp.spp;
 }
 
@@ -772,20 +775,21 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         }
         const float test = rng_next(rng);                                                    // main.cu:101
         uint32_t l;
-        if (last_sample(fp, p, l)) {
+        size_t fo;
+        if (last_sample(fp, p, l, fo)) {
             const uint32_t out = fp.aov_local ? l : global_pixel(fp, l);
             if (fp.albedo) {
                 const vec3 al = bsdf_albedo(bsdf);
-                fp.albedo[3 * out + 0] = al.x;
-                fp.albedo[3 * out + 1] = al.y;
-                fp.albedo[3 * out + 2] = al.z;
+                fp.albedo[fo + 3 * out + 0] = al.x;
+                fp.albedo[fo + 3 * out + 1] = al.y;
+                fp.albedo[fo + 3 * out + 2] = al.z;
             }
             if (fp.normal) {
-                fp.normal[3 * out + 0] = geo.normal.x;
-                fp.normal[3 * out + 1] = geo.normal.y;
-                fp.normal[3 * out + 2] = geo.normal.z;
+                fp.normal[fo + 3 * out + 0] = geo.normal.x;
+                fp.normal[fo + 3 * out + 1] = geo.normal.y;
+                fp.normal[fo + 3 * out + 2] = geo.normal.z;
             }
-            if (fp.test) fp.test[out] = test;
+            if (fp.test) fp.test[fo + out] = test;
         }
     } else if (hg.emitter >= 0) {  // main.cu:171-182
         const DevEmitter &e = sc.areas[hg.emitter];
@@ -908,11 +912,12 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
         }
         const float test = rng_next(rng);
         uint32_t l;
-        if (last_sample(fp, p, l)) {
+        size_t fo;
+        if (last_sample(fp, p, l, fo)) {
             const uint32_t out = fp.aov_local ? l : global_pixel(fp, l);
-            if (fp.albedo) fp.albedo[3 * out] = fp.albedo[3 * out + 1] = fp.albedo[3 * out + 2] = 0.f;
-            if (fp.normal) fp.normal[3 * out] = fp.normal[3 * out + 1] = fp.normal[3 * out + 2] = 0.f;
-            if (fp.test) fp.test[out] = test;
+            if (fp.albedo) fp.albedo[fo + 3 * out] = fp.albedo[fo + 3 * out + 1] = fp.albedo[fo + 3 * out + 2] = 0.f;
+            if (fp.normal) fp.normal[fo + 3 * out] = fp.normal[fo + 3 * out + 1] = fp.normal[fo + 3 * out + 2] = 0.f;
+            if (fp.test) fp.test[fo + out] = test;
         }
         st_ps(ps.rad + p, f4(L, 0.f));
     } else if (sc.has_env) {
