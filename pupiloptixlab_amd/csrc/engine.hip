@@ -578,11 +578,17 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
                            (cont_seed && pt->pipe_run >= 1);
     uint32_t K = 1, G = 1;
     if (may_pipe) {
-        // frame groups: renders smaller than PUPIL_PIPE_GROUP_PATHS (one rank's tiles at the
-        // 1-spp OnRun cadence) batch G consecutive frames per ring slot, so each traversal
-        // launch carries enough rays to amortise its tail; the renders whose frame an earlier
-        // render already completed only accumulate it
-        G = (uint32_t)std::min(64.0, std::max(1.0, std::ceil(pt->pipe_group_paths / (double)np)));
+        // frame groups: 1-spp renders (the OnRun cadence) smaller than PUPIL_PIPE_GROUP_PATHS
+        // (one rank's tiles, small films) batch G consecutive frames per ring slot, so each
+        // traversal launch carries enough rays to amortise its tail; the renders whose frame an
+        // earlier render already completed only accumulate it.  Batched renders (spp > 1, the
+        // bench's progressive steps) keep one frame per slot (PUPIL_PIPE_GROUP_ALL=1: group them too)
+        static const bool group_all = [] {
+            const char *e = std::getenv("PUPIL_PIPE_GROUP_ALL");
+            return e && std::atoi(e) != 0;
+        }();
+        if (launch->spp == 1 || group_all)
+            G = (uint32_t)std::min(64.0, std::max(1.0, std::ceil(pt->pipe_group_paths / (double)np)));
         K = pt->pipe_limit ? std::min(pt->pipe_limit, D) : D;
         constexpr double kPathBytes = 8 * 16 + 2 + 4 + 8 + 1;  // PathState + bins + nxsh + partition scratch
         K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::floor(pt->pipe_budget / ((double)G * np * kPathBytes))));

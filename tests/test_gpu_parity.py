@@ -566,6 +566,8 @@ def test_pipelined_onrun_sequence(case, monkeypatch):
     # one frame per ring slot unless grouped (4 frames of this render size per slot)
     npaths = (2 * 16 * 16 if case == "tiles" else w.desc().width * w.desc().height) * spp  # tiles 1, 4 of 3 x 2
     monkeypatch.setenv("PUPIL_PIPE_GROUP_PATHS", str(4 * npaths - 1 if grouped else 1))
+    if grouped and spp > 1:
+        monkeypatch.setenv("PUPIL_PIPE_GROUP_ALL", "1")
     pt = PTPass(device=0)
     pt.set_scene(w)
     if case == "tiles":
