@@ -684,7 +684,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         const uint32_t gspp = nf.frames * fp.spp;         // its samples per pixel
         const uint32_t interleave = interleave0 && gspp > 1 ? gspp : 0u;
         if (inject) {
-            if (!(PUPIL_CAMGEN && pt->fresh())) {  // list shading generates the camera rays in the traversal
+            if (!(PUPIL_CAMGEN == 1 && pt->fresh())) {  // PUPIL_CAMGEN 1: the traversal generates the camera rays
                 FrameParams fg = fp;
                 fg.seed0 = nf.seed;
                 fg.num_paths = nfp;

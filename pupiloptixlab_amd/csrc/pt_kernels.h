@@ -169,9 +169,12 @@ struct TraceStats {
     unsigned long long *wave_times = nullptr;
 };
 
-// Camera rays generated inside the persistent traversal (no generate pass, no camera-ray
-// records): path p of the batch -> main.cu:53-75's ray for seed seed0 + p / num_local.
-// PUPIL_CAMGEN=0 (A/B builds): k_generate stores the camera rays and the kernels read them.
+// Camera rays of list renders (fresh paths), PUPIL_CAMGEN at build time:
+//   1: generated inside the persistent traversal's refill (no generate pass, no camera-ray
+//      records): path p of the batch -> main.cu:53-75's ray for seed seed0 + p / num_local;
+//   2: k_generate stores the direction only, the traversal takes the origin from the camera;
+//   0: k_generate stores origin and direction and the kernels read them (r03).
+// The bounce-0 shade of a fresh path recomputes its ray (1, 2) or reads it (0).
 #ifndef PUPIL_CAMGEN
 #define PUPIL_CAMGEN 1
 #endif

@@ -189,15 +189,15 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     float4 o, d;
                     if (MODE == kModeExtend) {
                         p = job.queue ? job.queue[i] : (job.spp ? (i % job.spp) * job.num_local + i / job.spp : i);
-                        if (PUPIL_CAMGEN && job.cam.on) {  // a camera ray, generated here (no k_generate pass)
+                        if (PUPIL_CAMGEN == 1 && job.cam.on) {  // a camera ray, generated here (no k_generate pass)
                             uint32_t pixel;
                             vec3 dir;
                             (void)camera_path(sc.camera, job.cam.width, job.cam.height, job.cam.pixel_map, job.num_local,
                                               job.cam.seed0, p, pixel, dir);
                             o = f4(camera_origin(sc.camera), 0.f);
                             d = f4(dir, 0.f);
-                        } else {
-                            o = ld_ps(ps.ray_o + p);
+                        } else {  // PUPIL_CAMGEN 2: k_generate stored the direction only, the origin is the camera's
+                            o = PUPIL_CAMGEN == 2 && job.cam.on ? f4(camera_origin(sc.camera), 0.f) : ld_ps(ps.ray_o + p);
                             d = ld_ps(ps.ray_d + p);
                         }
                         tmin = 0.001f;
@@ -209,7 +209,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         const uint32_t pl = job.spp ? (j % job.spp) * job.num_local + j / job.spp : j;
                         p = pl + job.ahead_base;
                         any = false;
-                        if (PUPIL_CAMGEN && job.cam.on) {  // generated here (no k_generate pass)
+                        if (PUPIL_CAMGEN == 1 && job.cam.on) {  // generated here (no k_generate pass)
                             uint32_t pixel;
                             vec3 dir;
                             (void)camera_path(sc.camera, job.cam.width, job.cam.height, job.cam.pixel_map, job.num_local,
@@ -217,7 +217,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                             o = f4(camera_origin(sc.camera), 0.f);
                             d = f4(dir, 0.f);
                         } else {
-                            o = ld_ps(ps.ray_o + p);
+                            o = PUPIL_CAMGEN == 2 && job.cam.on ? f4(camera_origin(sc.camera), 0.f) : ld_ps(ps.ray_o + p);
                             d = ld_ps(ps.ray_d + p);
                         }
                         tmin = 0.001f;
@@ -583,7 +583,8 @@ __global__ __launch_bounds__(kShadeBlock) void k_generate(DeviceScene sc, FrameP
     if (p >= fp.num_paths) return;
     vec3 dir;
     const uint32_t rng = fresh_path(sc, fp, p, fp.seed0, dir);
-    st_ps(ps.ray_o + p, f4(camera_origin(sc.camera), 0.f));
+    // PUPIL_CAMGEN 2, list renders: the traversal and the bounce-0 shade take the origin from the camera
+    if (!(PUPIL_CAMGEN == 2 && !full)) st_ps(ps.ray_o + p, f4(camera_origin(sc.camera), 0.f));
     st_ps(ps.ray_d + p, make_float4(dir.x, dir.y, dir.z, 0.f));
     if (!full) return;
     st_ps(ps.thr + p, make_float4(1.f, 1.f, 1.f, 0.f));
