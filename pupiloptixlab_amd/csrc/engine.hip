@@ -684,15 +684,12 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         const uint32_t gspp = nf.frames * fp.spp;         // its samples per pixel
         const uint32_t interleave = interleave0 && gspp > 1 ? gspp : 0u;
         if (inject) {
-            if (!(PUPIL_CAMGEN == 1 && pt->fresh())) {  // PUPIL_CAMGEN 1: the traversal generates the camera rays
-                FrameParams fg = fp;
-                fg.seed0 = nf.seed;
-                fg.num_paths = nfp;
-                launch_generate(pt->sc, fg, cx.view(nf.slot, cap_paths), s, !pt->fresh());
-            }
+            FrameParams fg = fp;
+            fg.seed0 = nf.seed;
+            fg.num_paths = nfp;
+            launch_generate(pt->sc, fg, cx.view(nf.slot, cap_paths), s, !pt->fresh());
             started += nfp;
         }
-        const CameraGen cam{pt->fresh() ? 1u : 0u, nf.seed, fp.width, fp.height, fp.pixel_map};
         if (had) {
             // the rays the previous iteration's shade spawned, over the slots in use, in
             // increasing path id: next (bit 0) and shadow (bit 1) lists -> q.nxsh
@@ -711,7 +708,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
             cx.tail_slot();
             if (inject)  // + the new group's camera rays, dequeued first in every chunk (pixel-major)
                 launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s, nfp, 0u,
-                                   (uint32_t)(nf.slot * cap_paths), interleave, nl, &cam);
+                                   (uint32_t)(nf.slot * cap_paths), interleave, nl);
             else
                 launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s);
             cx.ev1();
@@ -719,7 +716,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
             cx.ev0(0);
             cx.tail_slot();
             launch_extend(pt->sc, cx.view(nf.slot, cap_paths), q, nullptr, nullptr, nfp, pt->ovf, pt->ovf_threads,
-                          cx.tsp(), s, interleave, nl, &cam);
+                          cx.tsp(), s, interleave, nl);
             cx.ev1();
         }
         if (inject) {  // the group is in flight from here (ring_end covers it)
@@ -1002,8 +999,6 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
     if (const char *g = std::getenv("PUPIL_PIPE_PATHS")) pt->pipe_paths = std::max(1.0, std::atof(g));
     if (const char *g = std::getenv("PUPIL_PIPE_GROUP_PATHS")) pt->pipe_group_paths = std::max(1.0, std::atof(g));
-    // PUPIL_TRAVERSAL=fused: the if-if kernel (trace4_body FUSED) for the flat / world-mode BVH4
-    if (const char *tv = std::getenv("PUPIL_TRAVERSAL")) sc.trace_fused = std::strcmp(tv, "fused") == 0 ? 1u : 0u;
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     if (nodes4_count(pt) > kMaxNodes4)

@@ -169,22 +169,6 @@ struct TraceStats {
     unsigned long long *wave_times = nullptr;
 };
 
-// Camera rays of list renders (fresh paths), PUPIL_CAMGEN at build time:
-//   1: generated inside the persistent traversal's refill (no generate pass, no camera-ray
-//      records): path p of the batch -> main.cu:53-75's ray for seed seed0 + p / num_local;
-//   2: k_generate stores the direction only, the traversal takes the origin from the camera;
-//   0: k_generate stores origin and direction and the kernels read them (r03).
-// The bounce-0 shade of a fresh path recomputes its ray (1, 2) or reads it (0).
-#ifndef PUPIL_CAMGEN
-#define PUPIL_CAMGEN 1
-#endif
-struct CameraGen {
-    uint32_t on;
-    uint32_t seed0;
-    uint32_t width, height;
-    const uint32_t *pixel_map;  // local -> global pixel (null = identity)
-};
-
 // wavefront stages
 // full = false: only the camera rays (the list shade then treats the batch as fresh paths)
 void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, hipStream_t s, bool full);
@@ -192,8 +176,7 @@ void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathSta
 // a pixel on consecutive lanes (TraceJob::spp); 0 = path order
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
                    const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
-                   const TraceStats *stats, hipStream_t s, uint32_t interleave_spp = 0, uint32_t num_local = 0,
-                   const CameraGen *cam = nullptr);
+                   const TraceStats *stats, hipStream_t s, uint32_t interleave_spp = 0, uint32_t num_local = 0);
 // which paths a shade launch walks: the material-bin partition (q.bins), a range of path
 // ids (every path of a batch after its primary extend), the previous bounce's next list
 // (q.nxsh), or that next list followed by a range (pipelined frames: the extension rays of
@@ -216,8 +199,7 @@ void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState 
 // primary extend)
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                         const TraceStats *stats, hipStream_t s, uint32_t ahead_count = 0, uint32_t list_base = 0,
-                        uint32_t ahead_base = 0, uint32_t ahead_spp = 0, uint32_t ahead_local = 0,
-                        const CameraGen *cam = nullptr);
+                        uint32_t ahead_base = 0, uint32_t ahead_spp = 0, uint32_t ahead_local = 0);
 // running mean of the batch's frames into fp.accum / fp.frame; aov_src (or null): the
 // frame's AOVs from the slot scratch (3n albedo, 3n normal, n test floats) copied to the
 // outputs; clear_flags: zero the frame's flags bytes (its ring slot is free again)

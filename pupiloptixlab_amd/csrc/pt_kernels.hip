@@ -86,14 +86,7 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
 // instance each; entering one pushes the pending TLAS link and kReturnLink and
 // switches the box tests to the instance's object-space ray; popping
 // kReturnLink switches back.  Spheres are tested at their TLAS leaf.
-// FUSED (flat / world-mode nodes only, not TL): one work item per lane per iteration --
-// a node visit or one primitive record of the leaf the lane is in, both fetched as the
-// same 16-dword load -- instead of the while-while node and leaf phases.  The kernel is
-// latency bound (the waves of a SIMD mostly wait on their fetches), so every lane's next
-// item rides on each memory round trip: a lane that reaches a leaf no longer idles until
-// the wave leaves the node phase, nor the node lanes during the leaf phase.  Hits are
-// resolved by the (t, id) order, so the closest hit does not depend on the visit order.
-template <int MODE, bool ANY, bool STATS, bool TL, bool FUSED = false>
+template <int MODE, bool ANY, bool STATS, bool TL>
 __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathState &ps, const Queues &q,
                                             const TraceJob &job, int *ovf, uint32_t ovf_threads,
                                             const TraceStats &stats, int *s_ring) {
@@ -132,7 +125,6 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     RayPre r{};
     float tmin = MODE == kModeRays ? 0.f : 0.001f, tmax = 0.f, b1 = 0.f, b2 = 0.f;  // tmin: a constant outside kModeRays
     int node = kSentinel, leaf = 0;
-    uint32_t rec = 0, rec_end = 0;  // FUSED: the records [rec, rec_end) of the leaf being tested
     bool found = false;
     bool any = ANY;  // this lane's ray terminates on its first hit
     bool in_blas = false;  // TL: traversing an instance's BLAS
@@ -189,37 +181,18 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     float4 o, d;
                     if (MODE == kModeExtend) {
                         p = job.queue ? job.queue[i] : (job.spp ? (i % job.spp) * job.num_local + i / job.spp : i);
-                        if (PUPIL_CAMGEN == 1 && job.cam.on) {  // a camera ray, generated here (no k_generate pass)
-                            uint32_t pixel;
-                            vec3 dir;
-                            (void)camera_path(sc.camera, job.cam.width, job.cam.height, job.cam.pixel_map, job.num_local,
-                                              job.cam.seed0, p, pixel, dir);
-                            o = f4(camera_origin(sc.camera), 0.f);
-                            d = f4(dir, 0.f);
-                        } else {  // PUPIL_CAMGEN 2: k_generate stored the direction only, the origin is the camera's
-                            o = PUPIL_CAMGEN == 2 && job.cam.on ? f4(camera_origin(sc.camera), 0.f) : ld_ps(ps.ray_o + p);
-                            d = ld_ps(ps.ray_d + p);
-                        }
+                        o = ld_ps(ps.ray_o + p);
+                        d = ld_ps(ps.ray_d + p);
                         tmin = 0.001f;
                         tmax = kMaxDistance;
                     } else if (MODE == kModeMixedAhead && k < len_a) {
                         // a camera ray of the next render (generated into the other half of the
                         // path state): the primary extend's pixel-major dequeue, then the offset
                         const uint32_t j = lo_a + k;
-                        const uint32_t pl = job.spp ? (j % job.spp) * job.num_local + j / job.spp : j;
-                        p = pl + job.ahead_base;
+                        p = (job.spp ? (j % job.spp) * job.num_local + j / job.spp : j) + job.ahead_base;
                         any = false;
-                        if (PUPIL_CAMGEN == 1 && job.cam.on) {  // generated here (no k_generate pass)
-                            uint32_t pixel;
-                            vec3 dir;
-                            (void)camera_path(sc.camera, job.cam.width, job.cam.height, job.cam.pixel_map, job.num_local,
-                                              job.cam.seed0, pl, pixel, dir);
-                            o = f4(camera_origin(sc.camera), 0.f);
-                            d = f4(dir, 0.f);
-                        } else {
-                            o = PUPIL_CAMGEN == 2 && job.cam.on ? f4(camera_origin(sc.camera), 0.f) : ld_ps(ps.ray_o + p);
-                            d = ld_ps(ps.ray_d + p);
-                        }
+                        o = ld_ps(ps.ray_o + p);
+                        d = ld_ps(ps.ray_d + p);
                         tmin = 0.001f;
                         tmax = kMaxDistance;
                     } else if (kMixed) {
@@ -255,11 +228,6 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         leaf = node;
                         node = kSentinel;
                     }
-                    if (FUSED) {  // the whole scene is one leaf: test it first
-                        rec = leaf < 0 ? leaf_first(leaf) : 0u;
-                        rec_end = leaf < 0 ? rec + leaf_count(leaf) : 0u;
-                        leaf = 0;
-                    }
                     active = true;
                 }
             }
@@ -269,86 +237,8 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             if (drained) break;
             continue;
         }
-        // ---- FUSED: one node visit or one record test per lane
-        if (FUSED && active && !(any && found)) {
-            const bool in_leaf = rec < rec_end;
-            const float4 *src = in_leaf ? sc.prims + 3 * (size_t)rec
-                                        : reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(sc.nodes4) +
-                                                                            ((uint32_t)node << 6));
-            const float4 q0 = src[0], q1 = src[1], q2 = src[2];
-            float4 q3 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (!in_leaf) q3 = src[3];
-            // the next link of the lane: a leaf link opens its record range, else the node
-            auto take = [&](int link) {
-                if (link < 0) {
-                    rec = leaf_first(link);
-                    rec_end = rec + leaf_count(link);
-                    node = kSentinel;
-                } else {
-                    node = link;
-                }
-            };
-            if (in_leaf) {
-                uint32_t &np_cnt = kMixed && any ? npt_sh : npt;
-                if (STATS) np_cnt++;
-                const uint32_t ref = __float_as_uint(q0.w);
-                const uint32_t key = ref & ~kPrimSphereBit;
-                float t, h1 = 0.f, h2 = 0.f;
-                bool hit;
-                if (ref & kPrimSphereBit) {
-                    const DevInstance &in = sc.instances[__float_as_uint(q1.w)];
-                    hit = intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, t);
-                } else {
-                    hit = intersect_triangle(r, v3(q0.x, q0.y, q0.z), v3(q1.x, q1.y, q1.z), v3(q2.x, q2.y, q2.z), tmin,
-                                             tmax, t, h1, h2);
-                }
-                if (hit && (any || t < tmax || key < best_key)) {
-                    tmax = t;
-                    best_key = key;
-                    best_idx = rec;
-                    b1 = h1;
-                    b2 = h2;
-                    found = true;
-                }
-                rec++;
-                if (rec == rec_end && !(any && found)) take(st.pop());
-            } else {
-                Bvh4Node n;
-                __builtin_memcpy(reinterpret_cast<char *>(&n), &q0, 16);
-                __builtin_memcpy(reinterpret_cast<char *>(&n) + 16, &q1, 16);
-                __builtin_memcpy(reinterpret_cast<char *>(&n) + 32, &q2, 16);
-                __builtin_memcpy(reinterpret_cast<char *>(&n) + 48, &q3, 16);
-                if (STATS) {
-                    if (kMixed && any) nv_sh++;
-                    else nv++;
-                    const unsigned long long m = __ballot(true);
-                    if ((int)lane_id() == __ffsll((long long)m) - 1) {
-                        dg[0]++;
-                        dg[1] += (unsigned long long)__popcll(m);
-                    }
-                    bool dup = false;
-                    for (int j = 0; j < 64; j++) {
-                        const int nj = __shfl(node, j);
-                        if (j < (int)lane_id() && ((m >> j) & 1ull) && nj == node) dup = true;
-                    }
-                    n_unique += dup ? 0u : 1u;
-                }
-                float t[4];
-                int l[4];
-                visit4(n, r.o, r.idir, be, tmin, tmax, t, l);
-                if (t[0] == kInf) {
-                    take(st.pop());
-                } else {
-                    st.reserve3();
-                    st.push(l[3], t[3] != kInf);
-                    st.push(l[2], t[2] != kInf);
-                    st.push(l[1], t[1] != kInf);
-                    take(l[0]);
-                }
-            }
-        }
         // ---- traverse until this lane's ray terminates or it needs a leaf while others do too
-        if (!FUSED && active) {
+        if (active) {
             while ((uint32_t)node < (uint32_t)kSentinel) {
                 const Bvh4Node n = load_node4(sc, node);
                 if (STATS) {
@@ -453,7 +343,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 }
             }
         }
-        const bool done = active && ((node == kSentinel && leaf >= 0 && rec >= rec_end) || (any && found));
+        const bool done = active && ((node == kSentinel && leaf >= 0) || (any && found));
         // ---- retire
         if (MODE == kModeExtend || kMixed) {
             uint32_t bin = 0;
@@ -542,14 +432,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring);
 }
 
-// fused node / record steps (trace4_body FUSED; PUPIL_TRAVERSAL=fused)
-template <int MODE, bool ANY, bool STATS>
-__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4f(
-    DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
-    __shared__ int s_ring[kRing * kTraceBlock];
-    trace4_body<MODE, ANY, STATS, false, true>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring);
-}
-
 // two-level variant: 9 more live registers (object-space box ray, margin,
 // instance) -> one wave less per SIMD so the loop does not spill
 template <int MODE, bool ANY, bool STATS>
@@ -573,18 +455,25 @@ __device__ __forceinline__ uint32_t fresh_path(const DeviceScene &sc, const Fram
     uint32_t pixel;
     return camera_path(sc.camera, fp.width, fp.height, fp.pixel_map, fp.num_local, seed0, p, pixel, dir);
 }
+// the RNG alone (main.cu:53-55: the two film draws follow the init)
+__device__ __forceinline__ uint32_t fresh_rng_of(const FrameParams &fp, uint32_t p, uint32_t seed0) {
+    const uint32_t s = p / fp.num_local;
+    const uint32_t l = p - s * fp.num_local;
+    uint32_t rng = rng_init(fp.pixel_map ? fp.pixel_map[l] : l, seed0 + s);
+    (void)rng_next(rng);
+    (void)rng_next(rng);
+    return rng;
+}
 
 // full = 0 (list shading, PUPIL_FRESH_SHADE): only the camera ray is stored; the bounce-0
 // shade of the fresh paths takes throughput 1, radiance 0 and the RNG from fresh_path
-// instead of reading them (k_shade_all `fresh`).  With in-kernel camera rays
-// (CameraGen) list renders need no generate pass at all.
+// instead of reading them (k_shade_all `fresh`).
 __global__ __launch_bounds__(kShadeBlock) void k_generate(DeviceScene sc, FrameParams fp, PathState ps, uint32_t full) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= fp.num_paths) return;
     vec3 dir;
     const uint32_t rng = fresh_path(sc, fp, p, fp.seed0, dir);
-    // PUPIL_CAMGEN 2, list renders: the traversal and the bounce-0 shade take the origin from the camera
-    if (!(PUPIL_CAMGEN == 2 && !full)) st_ps(ps.ray_o + p, f4(camera_origin(sc.camera), 0.f));
+    st_ps(ps.ray_o + p, f4(camera_origin(sc.camera), 0.f));
     st_ps(ps.ray_d + p, make_float4(dir.x, dir.y, dir.z, 0.f));
     if (!full) return;
     st_ps(ps.thr + p, make_float4(1.f, 1.f, 1.f, 0.f));
@@ -604,8 +493,8 @@ struct HitGeo {
 // shading record (bvh_build.hip k_attrs: object-space vertices, normals, uvs).
 // ro_rec: the ray origin record, read only for a sphere hit (the triangle position is
 // interpolated from the vertices)
-__device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, const float4 *ro_rec, bool fresh,
-                                             vec3 rd, vec2 stale_uv) {
+__device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, const float4 *ro_rec, vec3 rd,
+                                             vec2 stale_uv) {
     HitGeo out;
     const uint32_t idx = __float_as_uint(h.w);
     // flat: idx = record in traversal order, which names the instance; two-level:
@@ -643,7 +532,7 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, c
     g.texcoord = stale_uv;
     uint32_t local = 0;
     if (sphere) {
-        const vec3 ro = PUPIL_CAMGEN && fresh ? camera_origin(sc.camera) : f3(ld_ps(ro_rec));
+        const vec3 ro = f3(ld_ps(ro_rec));
         g.position = ro + h.x * rd;
         const vec3 local_pos = xform_point(in.to_object, g.position);
         g.texcoord = sphere_texcoord(normalize(local_pos - v3(0.f)));
@@ -723,12 +612,12 @@ __device__ __forceinline__ const DevEmitter *select_emitter(const DeviceScene &s
 // VGPRs, one wave less per SIMD).
 // Last sample of its frame, and the local pixel (AOVs are written for the last sample);
 // `frame_off`: the AOV offset of the sample's frame within a ring slot's frame group.
-__device__ __forceinline__ bool last_sample(const FrameParams &fp, uint32_t p, uint32_t &l, size_t &frame_off) {
+__device__ __forceinline__ bool last_sample(const FrameParams &fp, uint32_t p, uint32_t &l, uint32_t &frame_off) {
     const uint32_t q = p / fp.num_local;
     l = p - q * fp.num_local;
-    const uint32_t g = fp.group > 1u ? fp.group : 1u;
-    frame_off = (size_t)((q % (g * fp.spp)) / fp.spp) * fp.aov_frame_stride;
-    return q % fp.spp + 1u == fp.spp;
+    const uint32_t s = q / fp.spp;  // frame (of the ring) the sample belongs to
+    frame_off = fp.aov_frame_stride ? (s % fp.group) * fp.aov_frame_stride : 0u;
+    return q - s * fp.spp + 1u == fp.spp;
 }
 
 // fresh: a path of the frame generated for this launch (bounce 0, throughput 1, radiance 0,
@@ -738,15 +627,9 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
                                               uint32_t p, bool fresh, uint32_t fresh_p, uint32_t fresh_seed0) {
     bool push_next = false, push_shadow = false;
     const float4 h = ld_ps(ps.hit + p);
-    // a fresh path's camera ray and RNG are recomputed (the traversal generated the ray too)
-    vec3 ray_d;
-    uint32_t fresh_rng = 0;
-    if (PUPIL_CAMGEN && fresh) fresh_rng = fresh_path(sc, fp, fresh_p, fresh_seed0, ray_d);
-    else ray_d = f3(ld_ps(ps.ray_d + p));
-    if (!PUPIL_CAMGEN && fresh) {  // A/B: the stored camera ray, the RNG recomputed
-        vec3 unused;
-        fresh_rng = fresh_path(sc, fp, fresh_p, fresh_seed0, unused);
-    }
+    const vec3 ray_d = f3(ld_ps(ps.ray_d + p));
+    // a fresh path's RNG after its camera draws, recomputed (k_generate stored only the ray)
+    const uint32_t fresh_rng = fresh ? fresh_rng_of(fp, fresh_p, fresh_seed0) : 0u;
     const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ld_ps(ps.misc + p);
     uint32_t rng = misc.x;
     const uint32_t flags = misc.y;
@@ -759,7 +642,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     vec3 L_add = v3(0.f);
     const vec2 stale_uv = v2(__uint_as_float(misc.z), __uint_as_float(misc.w));
 
-    HitGeo hg = reconstruct(sc, h, ps.ray_o + p, fresh, ray_d, stale_uv);
+    HitGeo hg = reconstruct(sc, h, ps.ray_o + p, ray_d, stale_uv);
     const DevInstance &in = sc.instances[hg.inst];
     const DevMaterial &mat = sc.materials[in.material];
     if (mat.twosided && dot(-ray_d, hg.g.normal) < 0.f) hg.g.normal = -hg.g.normal;  // geometry.h:316-320
@@ -776,7 +659,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         }
         const float test = rng_next(rng);                                                    // main.cu:101
         uint32_t l;
-        size_t fo;
+        uint32_t fo;
         if (last_sample(fp, p, l, fo)) {
             const uint32_t out = fp.aov_local ? l : global_pixel(fp, l);
             if (fp.albedo) {
@@ -796,8 +679,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
         const DevEmitter &e = sc.areas[hg.emitter];
         vec3 Le;
         float pdf_e;
-        emitter_eval_area(e, geo, PUPIL_CAMGEN && fresh ? camera_origin(sc.camera) : f3(ld_ps(ps.ray_o + p)), Le,
-                          pdf_e);
+        emitter_eval_area(e, geo, f3(ld_ps(ps.ray_o + p)), Le, pdf_e);
         if (!is_zero(pdf_e)) {
             const float mis = (flags >> 31) ? 1.f : mis_weight(prev_pdf, pdf_e * e.select_probability);
             L_add = T * Le * mis;
@@ -896,9 +778,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
 // env handling at main.cu:87-99 / 165-169).
 __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FrameParams &fp, const PathState &ps,
                                            uint32_t p, bool fresh, uint32_t fresh_p, uint32_t fresh_seed0) {
-    vec3 fresh_d = v3(0.f);
-    uint32_t fresh_rng = 0;
-    if (fresh) fresh_rng = fresh_path(sc, fp, fresh_p, fresh_seed0, fresh_d);
+    const uint32_t fresh_rng = fresh ? fresh_rng_of(fp, fresh_p, fresh_seed0) : 0u;
     const uint4 misc = fresh ? make_uint4(fresh_rng, 0u, 0u, 0u) : ld_ps(ps.misc + p);
     if ((misc.y & 0xFFFFFFu) == 0u) {
         float4 rad4 = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : ld_ps(ps.rad + p);
@@ -907,13 +787,12 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
         if (sc.has_env) {
             vec3 Le;
             float pdf;
-            if (PUPIL_CAMGEN && fresh) env_eval(*sc.env, camera_origin(sc.camera), fresh_d, Le, pdf);
-            else env_eval(*sc.env, f3(ld_ps(ps.ray_o + p)), f3(ld_ps(ps.ray_d + p)), Le, pdf);
+            env_eval(*sc.env, f3(ld_ps(ps.ray_o + p)), f3(ld_ps(ps.ray_d + p)), Le, pdf);
             L = L + Le;  // main.cu:185, no MIS on the camera ray
         }
         const float test = rng_next(rng);
         uint32_t l;
-        size_t fo;
+        uint32_t fo;
         if (last_sample(fp, p, l, fo)) {
             const uint32_t out = fp.aov_local ? l : global_pixel(fp, l);
             if (fp.albedo) fp.albedo[fo + 3 * out] = fp.albedo[fo + 3 * out + 1] = fp.albedo[fo + 3 * out + 2] = 0.f;
@@ -1072,13 +951,6 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
         else
             hipLaunchKernelGGL((k_trace4tl<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
                                ovf, ovf_threads, st);
-    } else if (sc.trace_fused) {
-        if (stats)
-            hipLaunchKernelGGL((k_trace4f<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
-                               ovf, ovf_threads, st);
-        else
-            hipLaunchKernelGGL((k_trace4f<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
-                               ovf, ovf_threads, st);
     } else if (stats) {
         hipLaunchKernelGGL((k_trace4<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
                            ovf_threads, st);
@@ -1125,21 +997,18 @@ void launch_generate(const DeviceScene &sc, const FrameParams &fp, const PathSta
 
 void launch_extend(const DeviceScene &sc, const PathState &ps, const Queues &q, const uint32_t *queue,
                    const uint32_t *queue_count, uint32_t static_count, int *ovf, uint32_t ovf_threads,
-                   const TraceStats *stats, hipStream_t s, uint32_t interleave_spp, uint32_t num_local,
-                   const CameraGen *cam) {
-    TraceJob job{queue,   queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min,
-                 nullptr, nullptr,     queue ? 0u : interleave_spp, num_local};
-    if (cam && !queue) job.cam = *cam;
+                   const TraceStats *stats, hipStream_t s, uint32_t interleave_spp, uint32_t num_local) {
+    const TraceJob job{queue,   queue_count, static_count, q.work + kWorkExtend, sc.trace_refill, sc.trace_node_min,
+                       nullptr, nullptr,     queue ? 0u : interleave_spp, num_local};
     launch_trace4<kModeExtend, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
 }
 
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                         const TraceStats *stats, hipStream_t s, uint32_t ahead_count, uint32_t list_base,
-                        uint32_t ahead_base, uint32_t ahead_spp, uint32_t ahead_local, const CameraGen *cam) {
-    TraceJob job{nullptr,       nullptr,   ahead_count,          q.work + kWorkExtend,
-                 sc.trace_refill, sc.trace_node_min, nullptr, nullptr,
-                 ahead_count ? ahead_spp : 0u, ahead_local, list_base, ahead_base};
-    if (cam && ahead_count) job.cam = *cam;
+                        uint32_t ahead_base, uint32_t ahead_spp, uint32_t ahead_local) {
+    const TraceJob job{nullptr,       nullptr,   ahead_count,          q.work + kWorkExtend,
+                       sc.trace_refill, sc.trace_node_min, nullptr, nullptr,
+                       ahead_count ? ahead_spp : 0u, ahead_local, list_base, ahead_base};
     if (ahead_count) launch_trace4<kModeMixedAhead, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
     else launch_trace4<kModeMixed, false>(sc, ps, q, job, ovf, ovf_threads, stats, s);
 }

@@ -139,7 +139,6 @@ struct DeviceScene {
     uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
     uint32_t num_cus;       // compute units of the device (persistent grid size)
     uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node
-    uint32_t trace_fused;     // flat / world BVH4 kernels: one node or record step per lane per iteration
     // per axis, max over every BVH4 node of |o| + 512 s (launch_node_bound after each build
     // and refit): the slab test's rounding bound is then one value per ray (pt_traverse.h
     // slab_error) instead of one per node visit

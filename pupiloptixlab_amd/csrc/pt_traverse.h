@@ -212,7 +212,6 @@ struct TraceJob {
     // as above) + ahead_base (the other half); both offsets are non-negative
     uint32_t list_base;
     uint32_t ahead_base;
-    CameraGen cam;  // cam.on: the camera rays (extend without a queue, the ahead share) are generated here
 };
 
 __device__ __forceinline__ float ubyte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xFFu); }

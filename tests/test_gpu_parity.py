@@ -149,13 +149,10 @@ def test_config1_cornellbox_named_size():
     assert rs["shadow_rays"] <= rs["shadow_rays_reference"] <= rs["primary_rays"] * (d.max_depth - 1)
 
 
-@pytest.mark.parametrize("accel", ["flat", "flat_fused", "two_level", "two_level_fused"])
+@pytest.mark.parametrize("accel", ["flat", "two_level"])
 def test_materials_parity_config2(accel, monkeypatch):
     """Config 2 (all seven BSDFs, spheres + boxes) at 192^2, 8 spp, depth 6; one flattened
-    BVH4, or a TLAS over the mesh and sphere instances; while-while or fused traversal."""
-    if accel.endswith("_fused"):
-        monkeypatch.setenv("PUPIL_TRAVERSAL", "fused")
-        accel = accel[: -len("_fused")]
+    BVH4, or a TLAS over the mesh and sphere instances."""
     monkeypatch.setenv("PUPIL_ACCEL", accel)
     p = scenes.cornell_materials_xml(os.path.join(TMP, "cbmat.xml"), 192, 192, 6)
     desc = World().load_scene(p).desc()
@@ -165,12 +162,9 @@ def test_materials_parity_config2(accel, monkeypatch):
     assert compare(gpu, ref, f"materials192x8-{accel}") == 192 * 192
 
 
-@pytest.mark.parametrize("refill", ["1", "16", "64", "fused"])
+@pytest.mark.parametrize("refill", ["1", "16", "64"])
 def test_sphere_field_parity(refill, monkeypatch):
-    if refill == "fused":
-        monkeypatch.setenv("PUPIL_TRAVERSAL", "fused")
-    else:
-        monkeypatch.setenv("PUPIL_REFILL", refill)
+    monkeypatch.setenv("PUPIL_REFILL", refill)
     w = scenes.sphere_field(27, 240, 136, 4, seed=3)
     desc = w.desc()
     gpu = render_gpu(desc, 2)
@@ -206,19 +200,12 @@ def test_deep_paths_parity():
 
 # (PUPIL_REFILL, PUPIL_NODE_MIN) of the persistent BVH4 kernel: refill thresholds from one idle lane to a
 # whole wave, node-phase exits from one lane to the whole wave
-TRAVERSALS = [("1", "8"), ("16", "8"), ("16", "1"), ("24", "64"), ("64", "8"), ("1", "fused"), ("16", "fused"),
-              ("64", "fused")]
+TRAVERSALS = [("1", "8"), ("16", "8"), ("16", "1"), ("24", "64"), ("64", "8")]
 
 
 def _set_traversal(monkeypatch, refill, node_min):
-    """(refill, node_min) of the while-while kernel, or (refill, "fused"): the if-if kernel"""
     monkeypatch.setenv("PUPIL_REFILL", refill)
-    if node_min == "fused":
-        monkeypatch.setenv("PUPIL_TRAVERSAL", "fused")
-        monkeypatch.delenv("PUPIL_NODE_MIN", raising=False)
-    else:
-        monkeypatch.delenv("PUPIL_TRAVERSAL", raising=False)
-        monkeypatch.setenv("PUPIL_NODE_MIN", node_min)
+    monkeypatch.setenv("PUPIL_NODE_MIN", node_min)
 
 
 def _trace(desc, rays, any_hit=0, tmin=0.001, tmax=1e16):
@@ -1017,8 +1004,7 @@ def test_shade_list_modes_parity(mode, monkeypatch):
         (rs["extension_rays"], rs["shadow_rays"], rs["shadow_rays_reference"])
 
 
-@pytest.mark.parametrize("family", ["bvh4", "bvh4_refill1", "bvh4_fused", "two_level_world", "two_level_world_fused",
-                                    "two_level_object"])
+@pytest.mark.parametrize("family", ["bvh4", "bvh4_refill1", "two_level_world", "two_level_object"])
 def test_persistent_queue_accounting(family, monkeypatch):
     """Every persistent traversal family hands out each listed ray exactly once: per
     launch, the items the XCD dequeue heads handed out = the lanes activated with them =
@@ -1030,8 +1016,6 @@ def test_persistent_queue_accounting(family, monkeypatch):
 
     if family == "bvh4_refill1":
         monkeypatch.setenv("PUPIL_REFILL", "1")
-    if family.endswith("_fused"):
-        monkeypatch.setenv("PUPIL_TRAVERSAL", "fused")
     if family.startswith("two_level"):
         monkeypatch.setenv("PUPIL_ACCEL", "two_level")
         monkeypatch.setenv("PUPIL_TL_MODE", "object" if family == "two_level_object" else "world")
