@@ -671,7 +671,7 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     // braid 8 = TLAS over the nodes 8 levels below each instance root.  Config 5 with the GPU-built
     // TLAS and GPU refits (r03, profiles/r03_tlas_braid_ab.txt): braid 6 / 7 / 8 -> 434 / 445 / 415 ms
     // per step, instance update 1.4 / 1.5 / 1.9 ms, build 37 / 61 / 131-148 ms
-    if (const char *b = std::getenv("PUPIL_TL_BRAID")) acc.braid = (uint32_t)std::min(8, std::max(0, std::atoi(b)));
+    if (const char *b = std::getenv("PUPIL_TL_BRAID")) acc.braid = (uint32_t)std::min(12, std::max(0, std::atoi(b)));
     // BLAS per mesh shape that some instance uses
     std::vector<uint8_t> used(shapes.size(), 0);
     std::vector<uint32_t> shape_of(n);
