@@ -36,7 +36,7 @@ struct TwoLevelAccel {
     // structure is one BVH4 the flat traversal kernels walk (no ray transform, no
     // return markers, the flat kernel's occupancy).  HBM pays one BLAS copy per instance.
     bool world = false;
-    uint32_t braid = 8;  // PUPIL_TL_BRAID
+    uint32_t braid = 10;  // PUPIL_TL_BRAID
     Bvh4Node *wnodes = nullptr;  // [0, tlas_cap) TLAS, then the per-instance world BLAS copies
     float *d_wbox = nullptr;     // world box of every copied node (6 floats)
     uint32_t num_wnodes = 0;

@@ -670,7 +670,10 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     acc.world = !(mode && std::strcmp(mode, "object") == 0);
     // braid 8 = TLAS over the nodes 8 levels below each instance root.  Config 5 with the GPU-built
     // TLAS and GPU refits (r03, profiles/r03_tlas_braid_ab.txt): braid 6 / 7 / 8 -> 434 / 445 / 415 ms
-    // per step, instance update 1.4 / 1.5 / 1.9 ms, build 37 / 61 / 131-148 ms
+    // per step, instance update 1.4 / 1.5 / 1.9 ms, build 37 / 61 / 131-148 ms.  r04 (two alternating
+    // rounds, profiles/r04_config5_braid_ab.txt): braid 8 / 10 / 11 / 12 -> 402 / 392-395 / 398-400 /
+    // 397-398 ms per step, 37.1 / 35.6 / 36.5 / 36.5 node visits per ray, update 2.0 / 3.0 / 3.1 / 3.4 ms,
+    // build 138 / 277-290 / 311-321 / 333-336 ms: braid 10 is the default
     if (const char *b = std::getenv("PUPIL_TL_BRAID")) acc.braid = (uint32_t)std::min(12, std::max(0, std::atoi(b)));
     // BLAS per mesh shape that some instance uses
     std::vector<uint8_t> used(shapes.size(), 0);
