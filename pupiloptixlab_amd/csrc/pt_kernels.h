@@ -153,6 +153,14 @@ __device__ __forceinline__ void st_ps(uint4 *a, uint4 v) {
 #endif
 }
 
+// persistent traversal: the path id, the best hit's record index and barycentrics in LDS, the
+// ray direction reloaded where needed, the overflow column recomputed on a spill (r04: 2 / 1
+// VGPR spills instead of 4 / 5, -1.8 % per launch, profiles/r04_trim_state_ab.txt; A/B
+// builds: -DPUPIL_TRIM=0)
+#ifndef PUPIL_TRIM
+#define PUPIL_TRIM 1
+#endif
+
 // shade: a path that spawns no extension ray skips its dead thr / misc stores, and rad is
 // stored only when the hit added emission (A/B builds: -DPUPIL_SHADE_SKIP=0)
 #ifndef PUPIL_SHADE_SKIP

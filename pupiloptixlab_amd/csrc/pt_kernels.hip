@@ -63,10 +63,10 @@ __device__ __forceinline__ vec3 camera_origin(const Camera &cam) { return v3(cam
 // Two-level: the object-space box ray of instance `in` (origin, reciprocal
 // direction) and its slab-test bound (pt_traverse.h slab_error_pad), which adds the
 // position margin at the exit of the instance's world box.
-__device__ __forceinline__ void enter_instance(const DevInstance &in, const RayPre &r, float tmax, const float bound[3],
-                                               vec3 &bo, vec3 &bi, vec3 &be) {
+__device__ __forceinline__ void enter_instance(const DevInstance &in, const RayPre &r, vec3 rd, float tmax,
+                                               const float bound[3], vec3 &bo, vec3 &bi, vec3 &be) {
     bo = xform_point(in.to_object, r.o);
-    const vec3 d = xform_vector(in.to_object, r.d);
+    const vec3 d = xform_vector(in.to_object, rd);
     const float tiny = 1e-30f;
     bi = v3(1.f / (fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x), 1.f / (fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y),
             1.f / (fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z));
@@ -76,7 +76,7 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
     te = fminf(te, fmaxf((in.wlo[2] - r.o.z) * r.idir.z, (in.whi[2] - r.o.z) * r.idir.z));
     te = fabsf(te) * 1.0001f;
     const float on = fmaxf(fmaxf(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z));
-    const float dn = fmaxf(fmaxf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
+    const float dn = fmaxf(fmaxf(fabsf(rd.x), fabsf(rd.y)), fabsf(rd.z));
     const float pad = __builtin_fmaf(in.margin[0], __builtin_fmaf(te, dn, on), in.margin[1]);
     be = v3(slab_error_pad(bo.x, bi.x, bound[0], pad), slab_error_pad(bo.y, bi.y, bound[1], pad),
             slab_error_pad(bo.z, bi.z, bound[2], pad));
@@ -89,7 +89,7 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
 template <int MODE, bool ANY, bool STATS, bool TL>
 __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathState &ps, const Queues &q,
                                             const TraceJob &job, int *ovf, uint32_t ovf_threads,
-                                            const TraceStats &stats, int *s_ring) {
+                                            const TraceStats &stats, int *s_ring, float *s_aux) {
     constexpr float kInf = __builtin_huge_valf();
     constexpr bool kMixed = MODE == kModeMixed || MODE == kModeMixedAhead;
     const uint32_t n_next = kMixed ? q.counts[kCntNext] : 0u;
@@ -98,7 +98,12 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     const uint32_t count = kMixed ? n_next + q.counts[kCntShadow] : (job.count_ptr ? *job.count_ptr : job.static_count);
     RingStack st;
     st.lds = s_ring + threadIdx.x;
+#if PUPIL_TRIM
+    st.ovf_blk = ovf + blockIdx.x * blockDim.x;
+    st.lds0 = s_ring;
+#else
     st.ovf = ovf + blockIdx.x * blockDim.x + threadIdx.x;
+#endif
     st.ovf_stride = ovf_threads;
     st.reset();
     uint32_t nv = 0, npt = 0, nv_sh = 0, npt_sh = 0;  // mixed: shadow-ray counts apart
@@ -121,9 +126,23 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     // must give handed = activated = retired = its list length, counters[23])
     uint32_t q_handed = 0, q_act = 0, q_ret = 0;
     if (STATS && stats.wave_times) t_start = __builtin_amdgcn_s_memrealtime();
-    uint32_t p = 0, best_key = 0, best_idx = kMissIndex;
+    uint32_t best_key = 0;
     RayPre r{};
-    float tmin = MODE == kModeRays ? 0.f : 0.001f, tmax = 0.f, b1 = 0.f, b2 = 0.f;  // tmin: a constant outside kModeRays
+    float tmin = MODE == kModeRays ? 0.f : 0.001f, tmax = 0.f;  // tmin: a constant outside kModeRays
+#if PUPIL_TRIM
+    // state read only at a hit update or at the retire lives in LDS (s_aux), not in VGPRs:
+    // the path id and the best hit's barycentrics
+    float &b1 = s_aux[threadIdx.x];
+    float &b2 = s_aux[kTraceBlock + threadIdx.x];
+    uint32_t &p = reinterpret_cast<uint32_t *>(s_aux)[2 * kTraceBlock + threadIdx.x];
+    uint32_t &best_idx = reinterpret_cast<uint32_t *>(s_aux)[3 * kTraceBlock + threadIdx.x];
+    b1 = b2 = 0.f;
+    p = 0;
+    best_idx = kMissIndex;
+#else
+    uint32_t p = 0, best_idx = kMissIndex;
+    float b1 = 0.f, b2 = 0.f;
+#endif
     int node = kSentinel, leaf = 0;
     bool found = false;
     bool any = ANY;  // this lane's ray terminates on its first hit
@@ -131,6 +150,19 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     uint32_t inst = 0;
     vec3 bo = v3(0.f), bi = v3(0.f);  // TL: box-test ray (object space inside a BLAS)
     vec3 be = v3(0.f);                // its slab-test bound (pt_traverse.h slab_error)
+    // the ray direction: kept in r.d, or (PUPIL_TRIM) reloaded for the rare sphere test /
+    // instance entry instead of being held across the loop
+    auto ray_dir = [&]() -> vec3 {
+#if PUPIL_TRIM
+        if (MODE == kModeRays) {
+            const float *r8 = job.rays + 8 * (size_t)p;
+            return v3(r8[3], r8[4], r8[5]);
+        }
+        return f3(any ? ld_ps(ps.sh_d + p) : ld_ps(ps.ray_d + p));
+#else
+        return r.d;
+#endif
+    };
     for (;;) {
         // ---- refill idle lanes (one atomic per wave)
         const unsigned long long idle = __ballot(!active);
@@ -293,7 +325,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     if (in.kind == PUPIL_SHAPE_SPHERE) {
                         if (STATS) np_cnt++;
                         float ts;
-                        if (intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, ts)) {
+                        if (intersect_unit_sphere(in.to_object, r.o, ray_dir(), tmin, tmax, ts)) {
                             if (any) {
                                 found = true;
                                 break;
@@ -311,7 +343,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         st.push(kReturnLink, true);
                         in_blas = true;
                         inst = id;
-                        enter_instance(in, r, tmax, sc.node_bound, bo, bi, be);
+                        enter_instance(in, r, ray_dir(), tmax, sc.node_bound, bo, bi, be);
                         node = in.blas_root;
                         leaf = 0;
                         if (node < 0) {
@@ -325,7 +357,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                                                  found, any))
                         break;
                 } else if (intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, np_cnt,
-                                                     found, any)) {
+                                                     found, any, ray_dir)) {
                     break;
                 }
                 leaf = node;
@@ -429,7 +461,8 @@ template <int MODE, bool ANY, bool STATS>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4(
     DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
     __shared__ int s_ring[kRing * kTraceBlock];
-    trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring);
+    __shared__ float s_aux[PUPIL_TRIM ? 4 * kTraceBlock : 1];
+    trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux);
 }
 
 // two-level variant: 9 more live registers (object-space box ray, margin,
@@ -438,7 +471,8 @@ template <int MODE, bool ANY, bool STATS>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimdTL))) void k_trace4tl(
     DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
     __shared__ int s_ring[kRing * kTraceBlock];
-    trace4_body<MODE, ANY, STATS, true>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring);
+    __shared__ float s_aux[PUPIL_TRIM ? 4 * kTraceBlock : 1];
+    trace4_body<MODE, ANY, STATS, true>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux);
 }
 
 

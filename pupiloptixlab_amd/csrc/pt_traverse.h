@@ -21,10 +21,13 @@ __device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, 
 
 // Leaf intersection (flattened BVH4 and two-level world mode).  any = terminate on the first
 // hit (shadow ray); a compile-time constant except in the mixed persistent kernel.
-template <bool STATS>
+// dirf(): the ray direction, for sphere records only (the traversal may reload it instead of
+// keeping it live, PUPIL_TRIM)
+template <bool STATS, typename DirF>
 __device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
                                                    float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
-                                                   float &bb2, uint32_t &prims_tested, bool &found, bool any) {
+                                                   float &bb2, uint32_t &prims_tested, bool &found, bool any,
+                                                   DirF dirf) {
     const uint32_t first = leaf_first(leaf);
     const uint32_t count = leaf_count(leaf);
     for (uint32_t i = first; i < first + count; i++) {
@@ -42,7 +45,7 @@ __device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const 
         bool hit;
         if (ref & kPrimSphereBit) {
             const DevInstance &in = sc.instances[__float_as_uint(b.w)];
-            hit = intersect_unit_sphere(in.to_object, r.o, r.d, tmin, tmax, t);
+            hit = intersect_unit_sphere(in.to_object, r.o, dirf(), tmin, tmax, t);
         } else {
             hit = intersect_triangle(r, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), tmin, tmax, t, b1,
                                      b2);
@@ -132,7 +135,20 @@ static_assert((kRing & (kRing - 1)) == 0, "ring size must be a power of two");
 
 struct RingStack {
     int *lds;  // this lane's column (stride kTraceBlock)
+#if PUPIL_TRIM
+    // the overflow column is found from the block's base and the lane's LDS column only
+    // when the ring spills or refills (no 64-bit per-lane pointer held across the loop)
+    int *ovf_blk;       // this block's first overflow column (uniform)
+    const int *lds0;    // the block's ring base (uniform)
+    __device__ __forceinline__ int *ovf_col() {
+        uint32_t lane;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"((uint32_t)(lds - lds0)));  // not hoisted out of the loop
+        return ovf_blk + lane;
+    }
+#else
     int *ovf;  // this lane's overflow column (stride ovf_stride)
+    __device__ __forceinline__ int *ovf_col() { return ovf; }
+#endif
     uint32_t ovf_stride;
     int sp;   // logical entries [0, sp)
     int bot;  // entries [0, bot) live in ovf, [bot, sp) in the ring
@@ -144,6 +160,7 @@ struct RingStack {
     // level + 2 per instance entry), so the guard below never triggers.
     __device__ __forceinline__ void reserve3() {
         if (sp + 3 - bot > kRing && bot + kSpill <= kStackOvf) {
+            int *ovf = ovf_col();
 #pragma unroll
             for (int k = 0; k < kSpill; k++) ovf[(uint32_t)(bot + k) * ovf_stride] = slot(bot + k);
             bot += kSpill;
@@ -158,6 +175,7 @@ struct RingStack {
         sp--;
         if (sp < bot) {
             bot -= kSpill;
+            const int *ovf = ovf_col();
 #pragma unroll
             for (int k = 0; k < kSpill; k++) slot(bot + k) = ovf[(uint32_t)(bot + k) * ovf_stride];
         }
