@@ -16,30 +16,13 @@
 
 #include "pt_scene.h"
 
-#ifndef PUPIL_KPACK  // A/B builds: the shear axes packed into one register
-#define PUPIL_KPACK 0
-#endif
-
 namespace pupil {
 
 struct RayPre {
     vec3 o, d;
     vec3 idir;  // for slab tests
-#if PUPIL_KPACK
-    // shear axes kx | ky << 2 | kz << 4 in one register, unpacked at each triangle test (the
-    // unpack is volatile asm, so the compiler cannot hoist three unpacked registers back out)
-    uint32_t kp;
+    int kx, ky, kz;
     float Sx, Sy, Sz;
-    PT_D int kx() const { uint32_t v; asm volatile("v_bfe_u32 %0, %1, 0, 2" : "=v"(v) : "v"(kp)); return (int)v; }
-    PT_D int ky() const { uint32_t v; asm volatile("v_bfe_u32 %0, %1, 2, 2" : "=v"(v) : "v"(kp)); return (int)v; }
-    PT_D int kz() const { uint32_t v; asm volatile("v_bfe_u32 %0, %1, 4, 2" : "=v"(v) : "v"(kp)); return (int)v; }
-#else
-    int kx_, ky_, kz_;
-    float Sx, Sy, Sz;
-    PT_HD int kx() const { return kx_; }
-    PT_HD int ky() const { return ky_; }
-    PT_HD int kz() const { return kz_; }
-#endif
 };
 
 PT_HD float comp(vec3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
@@ -65,13 +48,9 @@ PT_HD RayPre ray_pre(vec3 o, vec3 d) {
         kx = ky;
         ky = t;
     }
-#if PUPIL_KPACK
-    r.kp = (uint32_t)kx | (uint32_t)ky << 2 | (uint32_t)kz << 4;
-#else
-    r.kx_ = kx;
-    r.ky_ = ky;
-    r.kz_ = kz;
-#endif
+    r.kx = kx;
+    r.ky = ky;
+    r.kz = kz;
     const float dz = comp(d, kz);
     r.Sx = comp(d, kx) / dz;
     r.Sy = comp(d, ky) / dz;
@@ -83,14 +62,13 @@ PT_HD RayPre ray_pre(vec3 o, vec3 d) {
 PT_HD bool intersect_triangle(const RayPre &r, vec3 v0, vec3 v1, vec3 v2, float tmin, float tmax, float &t_out,
                               float &b1, float &b2) {
     const vec3 A = v0 - r.o, B = v1 - r.o, C = v2 - r.o;
-    const int kx = r.kx(), ky = r.ky(), kz = r.kz();
-    const float Akz = comp(A, kz), Bkz = comp(B, kz), Ckz = comp(C, kz);
-    const float Ax = comp(A, kx) - r.Sx * Akz;
-    const float Ay = comp(A, ky) - r.Sy * Akz;
-    const float Bx = comp(B, kx) - r.Sx * Bkz;
-    const float By = comp(B, ky) - r.Sy * Bkz;
-    const float Cx = comp(C, kx) - r.Sx * Ckz;
-    const float Cy = comp(C, ky) - r.Sy * Ckz;
+    const float Akz = comp(A, r.kz), Bkz = comp(B, r.kz), Ckz = comp(C, r.kz);
+    const float Ax = comp(A, r.kx) - r.Sx * Akz;
+    const float Ay = comp(A, r.ky) - r.Sy * Akz;
+    const float Bx = comp(B, r.kx) - r.Sx * Bkz;
+    const float By = comp(B, r.ky) - r.Sy * Bkz;
+    const float Cx = comp(C, r.kx) - r.Sx * Ckz;
+    const float Cy = comp(C, r.ky) - r.Sy * Ckz;
     float U = Cx * By - Cy * Bx;
     float V = Ax * Cy - Ay * Cx;
     float W = Bx * Ay - By * Ax;
