@@ -328,7 +328,9 @@ void pupil_pt_destroy(pupil_pt *pt);
 int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out, int any_hit);
 /* copies the flattened BVH4 the traversal kernels read (64-B quantized nodes, 12-float
  * world-space primitive records, root link) to host memory, for the CPU baseline that
- * traverses the same arrays.  Call with nodes = records = NULL for the
+ * traverses the same arrays.  Records are the device's record slots (leaf
+ * links name slots; every leaf starts on an even slot), 12 floats each; a hole slot between
+ * leaves has all bits of its first record's w set.  Call with nodes = records = NULL for the
  * counts.  PUPIL_ERR_UNSUPPORTED for the two-level structure. */
 int pupil_pt_export_bvh4(pupil_pt *pt, uint32_t *num_nodes, void *nodes, uint32_t *num_records, float *records,
                          int32_t *root_link);

@@ -1712,6 +1712,10 @@ int oracle_set_bvh4(oracle_scene *s, uint32_t num_nodes, const void *nodes, uint
     for (uint32_t i = 0; i < num_records; i++) {
         uint32_t bits;
         std::memcpy(&bits, &records[12 * i + 3], 4);
+        if (bits == 0xFFFFFFFFu) {  // a hole slot between leaves (no leaf names it)
+            sc.q4_rec_prim[i] = 0xFFFFFFFFu;
+            continue;
+        }
         bits &= 0x7FFFFFFFu;  // sphere bit
         if (bits >= sc.prims.size()) return -1;
         sc.q4_rec_prim[i] = bits;

@@ -98,16 +98,21 @@ __global__ __launch_bounds__(kBlock) void k_world_records(const DevInstance *ins
     const uint32_t id = list[blockIdx.y];
     const DevInstance &in = insts[id];
     if (in.kind == PUPIL_SHAPE_SPHERE) return;
-    const uint32_t n = num_prims[id];
-    const uint32_t base = (uint32_t)((int32_t)in.attr_base);  // the shape's first BLAS record
+    const uint32_t n = num_prims[id];  // the shape's BLAS record slots
+    const uint32_t base = in.rec_base;  // the shape's first BLAS record slot
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        const float4 a = obj[3 * (size_t)(base + j) + 0];
-        const float4 b = obj[3 * (size_t)(base + j) + 1];
-        const float4 c = obj[3 * (size_t)(base + j) + 2];
+        const float4 a = obj[kRecF4 * (size_t)(base + j) + 0];
+        const float4 b = obj[kRecF4 * (size_t)(base + j) + 1];
+        const float4 c = obj[kRecF4 * (size_t)(base + j) + 2];
+        float4 *o = wrec + kRecF4 * (size_t)((int64_t)base + j + in.wrec_delta);
+        if (__float_as_uint(a.w) == kRecHole) {  // a hole slot stays a hole
+            o[0] = a;
+            o[1] = b;
+            continue;
+        }
         const vec3 w0 = xform_point(in.to_world, v3(a.x, a.y, a.z));
         const vec3 w1 = xform_point(in.to_world, v3(b.x, b.y, b.z));
         const vec3 w2 = xform_point(in.to_world, v3(c.x, c.y, c.z));
-        float4 *o = wrec + 3 * (size_t)((int64_t)base + j + in.wrec_delta);
         // flat record format (bvh_build.hip k_prim_setup): a.w = global id, b.w = instance, c.w = material bin
         o[0] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(in.prim_offset + __float_as_uint(a.w)));
         o[1] = make_float4(w1.x, w1.y, w1.z, __uint_as_float(id));
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void k_world_refit(const DevInstance *insts
                 const uint32_t first = (uint32_t)((int64_t)leaf_first(l) + in.wrec_delta), cnt = leaf_count(l);
                 for (uint32_t r = first; r < first + cnt; r++)
                     for (int v = 0; v < 3; v++) {
-                        const float4 p = wrec[3 * (size_t)r + v];
+                        const float4 p = wrec[kRecF4 * (size_t)r + v];
                         bl[0] = fminf(bl[0], p.x);
                         bl[1] = fminf(bl[1], p.y);
                         bl[2] = fminf(bl[2], p.z);
@@ -211,8 +216,8 @@ __global__ __launch_bounds__(kBlock) void k_tlas_refit(const uint32_t *order, ui
                 }
             } else {
                 const uint32_t first = leaf_first(l), cnt = leaf_count(l);
-                if (__float_as_uint(wrec[3 * (size_t)first].w) & kPrimSphereBit) {
-                    const uint32_t i = __float_as_uint(wrec[3 * (size_t)first + 1].w);
+                if (__float_as_uint(wrec[kRecF4 * (size_t)first].w) & kPrimSphereBit) {
+                    const uint32_t i = __float_as_uint(wrec[kRecF4 * (size_t)first + 1].w);
                     for (int a = 0; a < 3; a++) {
                         bl[a] = inst_box[6 * (size_t)i + a];
                         bh[a] = inst_box[6 * (size_t)i + 3 + a];
@@ -220,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void k_tlas_refit(const uint32_t *order, ui
                 } else {
                     for (uint32_t r = first; r < first + cnt; r++)
                         for (int c = 0; c < 3; c++) {
-                            const float4 q = wrec[3 * (size_t)r + c];
+                            const float4 q = wrec[kRecF4 * (size_t)r + c];
                             bl[0] = fminf(bl[0], q.x);
                             bl[1] = fminf(bl[1], q.y);
                             bl[2] = fminf(bl[2], q.z);
@@ -552,10 +557,14 @@ int rebuild_tlas(TwoLevelAccel &acc, std::vector<DevInstance> &insts, DevInstanc
         }
     }
     if (acc.world) {  // TLAS over the braided entries of every instance
-        uint32_t srec = acc.num_wprims;  // sphere records follow the mesh records, in instance order
+        // sphere records follow the mesh records, in instance order, one leaf (2 slots) each
+        uint32_t srec = acc.num_wprims;
         std::vector<uint32_t> sphere_rec(n, 0);
         for (uint32_t i = 0; i < n; i++)
-            if (insts[i].kind == PUPIL_SHAPE_SPHERE) sphere_rec[i] = srec++;
+            if (insts[i].kind == PUPIL_SHAPE_SPHERE) {
+                sphere_rec[i] = srec;
+                srec += leaf_slots(1u);
+            }
         for (uint32_t id : changed)
             if (!world_entries(acc, insts[id], id, sphere_rec[id], s)) return -1;
         if (refit && refit_world_tlas(acc, s)) return 0;
@@ -683,9 +692,11 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         if (shape_of[i] != 0xFFFFFFFFu) used[shape_of[i]] = 1;
     }
     std::vector<BvhBuildOutput> blas(shapes.size());
-    std::vector<uint32_t> node_base(shapes.size(), 0), prim_base(shapes.size(), 0);
+    // prim_base: a shape's first primitive (shading records, one per primitive); rec_base: its
+    // first BLAS record slot (pt_scene.h kRecF4: leaves on even slots, holes between)
+    std::vector<uint32_t> node_base(shapes.size(), 0), prim_base(shapes.size(), 0), rec_base(shapes.size(), 0);
     acc.tlas_cap = std::max(1u, n);
-    uint32_t total_nodes = acc.tlas_cap, total_prims = 0, max_faces = 1;
+    uint32_t total_nodes = acc.tlas_cap, total_prims = 0, total_slots = 0, max_faces = 1;
     for (size_t k = 0; k < shapes.size(); k++)
         if (used[k]) max_faces = std::max(max_faces, shapes[k].num_faces);
     uint32_t *zeros = nullptr;
@@ -724,12 +735,14 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         }
         node_base[k] = total_nodes;
         prim_base[k] = total_prims;
+        rec_base[k] = total_slots;
         if (blas[k].level_start.size() < 2) acc.world = false;  // no level order (A/B node layouts): object mode
         total_nodes += blas[k].num_nodes4;
         total_prims += sh.num_faces;
+        total_slots += sh.num_faces ? blas[k].num_records : 0u;
     }
     if (!rc && (hipMalloc((void **)&acc.nodes4, sizeof(Bvh4Node) * total_nodes) != hipSuccess ||
-                hipMalloc((void **)&acc.prims, sizeof(float4) * 3 * (size_t)std::max(1u, total_prims)) != hipSuccess ||
+                hipMalloc((void **)&acc.prims, sizeof(float4) * kRecF4 * (size_t)std::max(1u, total_slots)) != hipSuccess ||
                 hipMalloc((void **)&acc.attrs, sizeof(float4) * kAttrStride * (size_t)std::max(1u, total_prims)) !=
                     hipSuccess ||
                 hipMalloc((void **)&acc.d_boxes, sizeof(uint32_t) * 6 * (size_t)n) != hipSuccess ||
@@ -743,7 +756,7 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         if (nf == 0) continue;
         if ((b.num_nodes4 && hipMemcpyAsync(acc.nodes4 + node_base[k], b.nodes4, sizeof(Bvh4Node) * b.num_nodes4,
                                             hipMemcpyDeviceToDevice, s) != hipSuccess) ||
-            hipMemcpyAsync(acc.prims + 3 * (size_t)prim_base[k], b.prims, sizeof(float4) * 3 * (size_t)nf,
+            hipMemcpyAsync(acc.prims + kRecF4 * (size_t)rec_base[k], b.prims, sizeof(float4) * kRecF4 * (size_t)b.num_records,
                            hipMemcpyDeviceToDevice, s) != hipSuccess ||
             hipMemcpyAsync(acc.attrs + kAttrStride * (size_t)prim_base[k], b.attrs, sizeof(float4) * kAttrStride * nf,
                            hipMemcpyDeviceToDevice, s) != hipSuccess) {
@@ -752,7 +765,7 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         }
         if (b.num_nodes4)
             hipLaunchKernelGGL(k_relink, dim3((b.num_nodes4 + kBlock - 1) / kBlock), dim3(kBlock), 0, s, acc.nodes4,
-                               b.num_nodes4, node_base[k], prim_base[k]);
+                               b.num_nodes4, node_base[k], rec_base[k]);
     }
     if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = -1;
     for (auto &b : blas) free_lbvh(b);
@@ -797,22 +810,24 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
             continue;
         }
         const uint32_t k = shape_of[i];
-        d.blas_root = shapes[k].num_faces ? rebase_link((int)blas[k].root_link4, node_base[k], prim_base[k])
+        d.blas_root = shapes[k].num_faces ? rebase_link((int)blas[k].root_link4, node_base[k], rec_base[k])
                                           : kTraverseDone;
         d.attr_base = prim_base[k];
-        d.wrec_delta = (int32_t)((int64_t)wbase - (int64_t)prim_base[k]);
-        wbase += shapes[k].num_faces;
+        d.rec_base = rec_base[k];
+        d.wrec_delta = (int32_t)((int64_t)wbase - (int64_t)rec_base[k]);
+        const uint32_t slots = shapes[k].num_faces ? blas[k].num_records : 0u;
+        wbase += slots;
         d.obj_nbase = node_base[k];
         d.obj_ncount = blas[k].num_nodes4;
         d.wnode_base = (uint32_t)wnodes;
         wnodes += blas[k].num_nodes4;
         verts[i] = shapes[k].num_vertices;
-        faces[i] = shapes[k].num_faces;
+        faces[i] = slots;  // the BLAS record slots k_world_records copies
         instance_margin(d, shapes[k].vmax);
     }
     int trc = 0;
     if (wbase >= (1ull << 31) ||
-        hipMalloc((void **)&acc.wprims, sizeof(float4) * 3 * (size_t)std::max<uint64_t>(1, wbase)) != hipSuccess ||
+        hipMalloc((void **)&acc.wprims, sizeof(float4) * kRecF4 * (size_t)std::max<uint64_t>(1, wbase)) != hipSuccess ||
         hipMalloc((void **)&acc.d_faces, sizeof(uint32_t) * n) != hipSuccess ||
         hipMemcpy(acc.d_faces, faces.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess) {
         free_two_level(acc);
@@ -831,13 +846,16 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         acc.inst_shape = shape_of;
         acc.shape_levels.assign(shapes.size(), {});
         for (size_t k = 0; k < shapes.size(); k++) acc.shape_levels[k] = blas[k].level_start;
-        std::vector<float4> sph(3 * spheres);
+        // one leaf (2 slots: the record, then a hole) per sphere
+        const float4 hole = make_float4(qfloat(kRecHole), qfloat(kRecHole), qfloat(kRecHole), qfloat(kRecHole));
+        std::vector<float4> sph(2 * kRecF4 * spheres, hole);
         uint32_t si = 0;
         for (uint32_t i = 0; i < n; i++) {
             if (insts[i].kind != PUPIL_SHAPE_SPHERE) continue;
-            sph[3 * si + 0] = make_float4(0.f, 0.f, 0.f, qfloat(insts[i].prim_offset | kPrimSphereBit));
-            sph[3 * si + 1] = make_float4(0.f, 0.f, 0.f, qfloat(i));
-            sph[3 * si + 2] = make_float4(0.f, 0.f, 0.f, qfloat(insts[i].bin));
+            float4 *r = sph.data() + 2 * kRecF4 * si;
+            r[0] = make_float4(0.f, 0.f, 0.f, qfloat(insts[i].prim_offset | kPrimSphereBit));
+            r[1] = make_float4(0.f, 0.f, 0.f, qfloat(i));
+            r[2] = make_float4(0.f, 0.f, 0.f, qfloat(insts[i].bin));
             si++;
         }
         float4 *grown = nullptr;
@@ -845,8 +863,9 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
             hipMalloc((void **)&acc.wnodes, sizeof(Bvh4Node) * (size_t)wnodes) != hipSuccess ||
             hipMalloc((void **)&acc.d_wbox, sizeof(float) * 6 * (size_t)wnodes) != hipSuccess ||
             hipMalloc((void **)&acc.d_tlas_order, sizeof(uint32_t) * (size_t)std::max(1u, acc.tlas_cap)) != hipSuccess ||
-            hipMalloc((void **)&grown, sizeof(float4) * 3 * (size_t)std::max<uint64_t>(1, wbase + spheres)) != hipSuccess ||
-            (spheres && hipMemcpy(grown + 3 * wbase, sph.data(), sizeof(float4) * sph.size(), hipMemcpyHostToDevice) !=
+            hipMalloc((void **)&grown, sizeof(float4) * kRecF4 * (size_t)std::max<uint64_t>(1, wbase + 2 * spheres)) !=
+                hipSuccess ||
+            (spheres && hipMemcpy(grown + kRecF4 * wbase, sph.data(), sizeof(float4) * sph.size(), hipMemcpyHostToDevice) !=
                             hipSuccess)) {
             if (grown) (void)hipFree(grown);
             free_two_level(acc);

@@ -824,14 +824,15 @@ __global__ void k_collapse_pick_sah(int items, const int *item_node, const int2 
 // object-space mesh, in one 128-B line instead of index + 3 x position / normal /
 // uv gathers:  [0] p0 | global id (+ sphere bit)  [1] p1 | instance  [2] p2 | n0.x
 // [3] n0.yz n1.xy  [4] n1.z n2.xyz  [5] t0 t1  [6] t2 | 0 0  [7] unused
-__global__ void k_attrs(int n, const uint32_t *sorted_vals, BvhBuildInput in, float4 *attrs) {
+__global__ void k_attrs(int n, const uint32_t *sorted_vals, const uint32_t *slot, BvhBuildInput in, float4 *attrs) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t prim = sorted_vals[i];
     const uint32_t inst_id = in.prim_inst[prim];
     const DevInstance &inst = in.instances[inst_id];
-    // object_space (BLAS): records in the mesh's own primitive order, found by primitive id
-    float4 *r = attrs + (size_t)kAttrStride * (in.object_space ? prim : (uint32_t)i);
+    // object_space (BLAS): records in the mesh's own primitive order, found by primitive id;
+    // flattened: by record slot (the hit index)
+    float4 *r = attrs + (size_t)kAttrStride * (in.object_space ? prim : slot[i]);
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     if (inst.kind == PUPIL_SHAPE_SPHERE) {
         r[0] = make_float4(0.f, 0.f, 0.f, __uint_as_float(prim | kPrimSphereBit));
@@ -864,13 +865,41 @@ __global__ void k_attrs(int n, const uint32_t *sorted_vals, BvhBuildInput in, fl
     r[7] = z;
 }
 
-__global__ void k_reorder(int n, const uint32_t *sorted_vals, const float4 *recs_in, float4 *recs_out) {
+__global__ void k_reorder(int n, const uint32_t *sorted_vals, const uint32_t *slot, const float4 *recs_in,
+                          float4 *recs_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t src = sorted_vals[i];
-    recs_out[3 * i + 0] = recs_in[3 * src + 0];
-    recs_out[3 * i + 1] = recs_in[3 * src + 1];
-    recs_out[3 * i + 2] = recs_in[3 * src + 2];
+    float4 *o = recs_out + (size_t)kRecF4 * slot[i];
+    o[0] = recs_in[3 * src + 0];
+    o[1] = recs_in[3 * src + 1];
+    o[2] = recs_in[3 * src + 2];
+}
+
+// Record slots (kRecF4): every leaf's slot count 2 ceil(c / 2) at its first primitive,
+// scanned, gives each leaf a first slot on a 128-B line
+__global__ void k_leaf_marks(const Bvh4Node *nodes, uint32_t m, unsigned long long *lsz) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const Bvh4Node nd = nodes[j];
+    for (int k = 0; k < 4; k++) {
+        const int l = nd.child[k];
+        if (l != kEmptyLink && l < 0) lsz[leaf_first(l)] = leaf_slots(leaf_count(l));
+    }
+}
+// each leaf's primitives -> their slots; its link now names its first slot
+__global__ void k_leaf_slots(Bvh4Node *nodes, uint32_t m, const unsigned long long *first_slot, uint32_t *slot) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    Bvh4Node nd = nodes[j];
+    for (int k = 0; k < 4; k++) {
+        const int l = nd.child[k];
+        if (l == kEmptyLink || l >= 0) continue;
+        const uint32_t f = leaf_first(l), c = leaf_count(l), fs = (uint32_t)first_slot[f];
+        for (uint32_t q = 0; q < c; q++) slot[f + q] = fs + q;
+        nd.child[k] = make_leaf(fs, c);
+    }
+    nodes[j] = nd;
 }
 
 template <typename T>
@@ -1077,8 +1106,6 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
     if (!err) err = dmalloc(&ranges, n);
     if (!err) err = dmalloc(&parent_internal, n);
     if (!err) err = dmalloc(&parent_leaf, n);
-    if (!err) err = dmalloc(&out.prims, 3 * (size_t)n);
-    if (!err) err = dmalloc(&out.attrs, (size_t)kAttrStride * n);
     if (err) {
         free_lbvh(out);
     } else {
@@ -1153,12 +1180,55 @@ int build_lbvh(const BvhBuildInput &in, BvhBuildOutput &out, uint32_t leaf_size,
         const bool leaf_root = (uint32_t)n <= leaf_size;
         const uint32_t *rec_vals = vi;
         const uint32_t nrec = (uint32_t)n;
+        // record slots: each leaf on a 128-B line (kRecF4); the links are rewritten to slots
+        uint32_t nslots = 0;
+        uint32_t *slot = nullptr;
+        unsigned long long *lsz = nullptr, *ssum = nullptr, *stot = nullptr;
+        const int per = kScanBlock * kScanItems;
+        const int nbs = (int)((nrec + per - 1) / per);
+        if (!err) err = dmalloc(&slot, nrec);
+        if (!err) err = dmalloc(&lsz, nrec);
+        if (!err) err = dmalloc(&ssum, nbs);
+        if (!err) err = dmalloc(&stot, 1);
+        if (!err && nbs > per) err = hipErrorInvalidValue;
+        if (!err) {
+            const uint32_t m = leaf_root ? 0u : out.num_nodes4;
+            err = hipMemsetAsync(lsz, 0, sizeof(unsigned long long) * nrec, s);
+            if (leaf_root && !err) {
+                const unsigned long long v = leaf_slots(nrec);
+                err = hipMemcpyAsync(lsz, &v, sizeof(v), hipMemcpyHostToDevice, s);
+            }
+            if (m) hipLaunchKernelGGL(k_leaf_marks, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, s, out.nodes4, m, lsz);
+            hipLaunchKernelGGL(k_scan64_blocks, dim3(nbs), dim3(kScanBlock), 0, s, lsz, (int)nrec, ssum);
+            hipLaunchKernelGGL(k_scan64_sums, dim3(1), dim3(kScanBlock), 0, s, ssum, nbs, stot);
+            hipLaunchKernelGGL(k_scan64_add, dim3((nrec + kBlock - 1) / kBlock), dim3(kBlock), 0, s, lsz, (int)nrec, ssum);
+            if (m) hipLaunchKernelGGL(k_leaf_slots, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, s, out.nodes4, m, lsz, slot);
+            if (leaf_root) {  // the root leaf: slots 0 .. n-1
+                std::vector<uint32_t> id(nrec);
+                for (uint32_t q = 0; q < nrec; q++) id[q] = q;
+                if (!err) err = hipMemcpyAsync(slot, id.data(), sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, s);
+                if (!err) err = hipStreamSynchronize(s);
+            }
+            unsigned long long tot = 0;
+            if (!err) err = hipMemcpyAsync(&tot, stot, sizeof(tot), hipMemcpyDeviceToHost, s);
+            if (!err) err = hipStreamSynchronize(s);
+            nslots = (uint32_t)tot;
+            if (!err && tot >= (1ull << 28)) err = hipErrorInvalidValue;  // leaf links hold 28-bit slots
+        }
+        if (!err) err = dmalloc(&out.prims, (size_t)kRecF4 * nslots);
+        if (!err) err = hipMemsetAsync(out.prims, 0xFF, sizeof(float4) * kRecF4 * (size_t)std::max(1u, nslots), s);
+        const size_t nattr = in.object_space ? (size_t)nrec : (size_t)nslots;
+        if (!err) err = dmalloc(&out.attrs, (size_t)kAttrStride * nattr);
         if (!err) {
             const uint32_t gr = (nrec + kBlock - 1) / kBlock;
-            hipLaunchKernelGGL(k_reorder, dim3(gr), dim3(kBlock), 0, s, (int)nrec, rec_vals, recs, out.prims);
-            hipLaunchKernelGGL(k_attrs, dim3(gr), dim3(kBlock), 0, s, (int)nrec, rec_vals, in, out.attrs);
+            hipLaunchKernelGGL(k_reorder, dim3(gr), dim3(kBlock), 0, s, (int)nrec, rec_vals, slot, recs, out.prims);
+            hipLaunchKernelGGL(k_attrs, dim3(gr), dim3(kBlock), 0, s, (int)nrec, rec_vals, slot, in, out.attrs);
         }
-        out.num_records = nrec;
+        (void)hipStreamSynchronize(s);
+        for (void *p : {(void *)slot, (void *)lsz, (void *)ssum, (void *)stot})
+            if (p) (void)hipFree(p);
+        if (err) free_lbvh(out);
+        out.num_records = nslots;
         if (n == 1 || leaf_root) out.depth4 = 1;  // the root is a leaf
         out.root_link4 = leaf_root ? (uint32_t)make_leaf(0u, (uint32_t)n) : 0u;
         if (!err) err = hipGetLastError();
@@ -1282,12 +1352,13 @@ namespace {
 
 // Records of the moved instance (b.w = instance) get its new world vertices, written
 // exactly as k_prim_setup writes them (global id in a.w: sphere bit + id).
-__global__ void k_refit_records(BvhBuildInput in, uint32_t n, float4 *recs, const uint8_t *moved) {
+__global__ void k_refit_records(BvhBuildInput in, uint32_t n, float4 *recs_base, const uint8_t *moved) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
-    const uint32_t id = __float_as_uint(recs[3 * r + 1].w);
-    if (!moved[id]) return;
-    const uint32_t gid = __float_as_uint(recs[3 * r].w) & ~kPrimSphereBit;
+    float4 *recs = recs_base + (size_t)kRecF4 * r;
+    const uint32_t id = __float_as_uint(recs[1].w);
+    if (id == kRecHole || !moved[id]) return;  // a hole slot, or an unmoved instance
+    const uint32_t gid = __float_as_uint(recs[0].w) & ~kPrimSphereBit;
     const DevInstance &inst = in.instances[id];
     if (inst.kind == PUPIL_SHAPE_SPHERE) {
         const float *m = inst.to_world;
@@ -1295,8 +1366,8 @@ __global__ void k_refit_records(BvhBuildInput in, uint32_t n, float4 *recs, cons
         const float ex = sqrtf(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * 1.001f;
         const float ey = sqrtf(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]) * 1.001f;
         const float ez = sqrtf(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]) * 1.001f;
-        recs[3 * r + 0] = make_float4(c.x, c.y, c.z, recs[3 * r].w);
-        recs[3 * r + 1] = make_float4(ex, ey, ez, recs[3 * r + 1].w);
+        recs[0] = make_float4(c.x, c.y, c.z, recs[0].w);
+        recs[1] = make_float4(ex, ey, ez, recs[1].w);
         return;
     }
     const uint32_t local = gid - inst.prim_offset;
@@ -1305,9 +1376,9 @@ __global__ void k_refit_records(BvhBuildInput in, uint32_t n, float4 *recs, cons
     const vec3 w0 = xform_point(inst.to_world, v3(P[3 * i0], P[3 * i0 + 1], P[3 * i0 + 2]));
     const vec3 w1 = xform_point(inst.to_world, v3(P[3 * i1], P[3 * i1 + 1], P[3 * i1 + 2]));
     const vec3 w2 = xform_point(inst.to_world, v3(P[3 * i2], P[3 * i2 + 1], P[3 * i2 + 2]));
-    recs[3 * r + 0] = make_float4(w0.x, w0.y, w0.z, recs[3 * r].w);
-    recs[3 * r + 1] = make_float4(w1.x, w1.y, w1.z, recs[3 * r + 1].w);
-    recs[3 * r + 2] = make_float4(w2.x, w2.y, w2.z, recs[3 * r + 2].w);
+    recs[0] = make_float4(w0.x, w0.y, w0.z, recs[0].w);
+    recs[1] = make_float4(w1.x, w1.y, w1.z, recs[1].w);
+    recs[2] = make_float4(w2.x, w2.y, w2.z, recs[2].w);
 }
 
 // One BVH4 level, bottom up: child boxes from the records under a leaf (exact; a
@@ -1332,7 +1403,7 @@ __global__ void k_refit_level(Bvh4Node *nodes, uint32_t lo, uint32_t hi, const f
                 }
             } else {
                 for (uint32_t r = leaf_first(l); r < leaf_first(l) + leaf_count(l); r++) {
-                    const float4 a = recs[3 * r], b = recs[3 * r + 1], c = recs[3 * r + 2];
+                    const float4 a = recs[kRecF4 * r], b = recs[kRecF4 * r + 1], c = recs[kRecF4 * r + 2];
                     if (__float_as_uint(a.w) & kPrimSphereBit) {
                         bl[0] = fminf(bl[0], a.x - b.x);
                         bl[1] = fminf(bl[1], a.y - b.y);
@@ -1377,7 +1448,7 @@ int refit_bvh4(const BvhBuildInput &in, BvhBuildOutput &out, const uint8_t *move
     (void)hipEventRecord(e0, s);
     hipError_t err = hipSuccess;
     {
-        const uint32_t n = in.num_prims;
+        const uint32_t n = out.num_records;  // record slots (holes are skipped)
         hipLaunchKernelGGL(k_refit_records, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, in, n, out.prims, moved);
         for (size_t L = out.level_start.size() - 1; L-- > 0;) {
             const uint32_t lo = out.level_start[L], hi = out.level_start[L + 1];

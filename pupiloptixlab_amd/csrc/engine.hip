@@ -907,7 +907,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     // world-space primitives (default: on config 5 it traces 1.08x faster than the
     // two-level world mode), or a TLAS over per-instance BLASes (PUPIL_ACCEL=two_level,
     // which bench.py selects for config 5: cheaper instance updates; automatic when
-    // the flattened primitive count would pass the flat build's 2^28 limit).  Both
+    // the flattened primitive count would pass the flat build's 2^27 limit).  Both
     // give bit-identical hits.
     {
         std::vector<uint32_t> uses(scene->num_shapes, 0), inst_shape(scene->num_instances);
@@ -918,13 +918,14 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
             const pupil_shape &sh = scene->shapes[inst_shape[i]];
             flat_prims += sh.kind == PUPIL_SHAPE_SPHERE ? 1u : sh.num_faces;
         }
-        pt->two_level = flat_prims >= (1ull << 28);
+        // leaf links hold 28-bit record slots, up to two per primitive (pt_scene.h kRecF4)
+        pt->two_level = flat_prims >= (1ull << 27);
         if (const char *a = std::getenv("PUPIL_ACCEL")) {
             if (std::strcmp(a, "flat") == 0) pt->two_level = false;
             if (std::strcmp(a, "two_level") == 0) pt->two_level = true;
         }
-        if (!pt->two_level && flat_prims >= (1ull << 28))
-            return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "flattened BVH limited to 2^28 primitives"));
+        if (!pt->two_level && flat_prims >= (1ull << 27))
+            return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "flattened BVH limited to 2^27 primitives"));
         if (pt->two_level) {
             std::vector<TwoLevelShape> tls(scene->num_shapes);
             for (uint32_t k = 0; k < scene->num_shapes; k++) {
@@ -1407,7 +1408,11 @@ int pupil_pt_export_bvh4(pupil_pt *pt, uint32_t *num_nodes, void *nodes, uint32_
         if (*num_nodes < nn || *num_records < nr) return fail(PUPIL_ERR_INVALID, "output too small");
         HIP_TRY(hipDeviceSynchronize());
         if (nodes && nn) HIP_TRY(hipMemcpy(nodes, pt->bvh.nodes4, sizeof(Bvh4Node) * nn, hipMemcpyDeviceToHost));
-        if (records && nr) HIP_TRY(hipMemcpy(records, pt->bvh.prims, sizeof(float4) * 3 * (size_t)nr, hipMemcpyDeviceToHost));
+        if (records && nr) {  // record slots as 12 floats each (the 4th float4 of a slot is unused)
+            std::vector<float4> h((size_t)kRecF4 * nr);
+            HIP_TRY(hipMemcpy(h.data(), pt->bvh.prims, sizeof(float4) * h.size(), hipMemcpyDeviceToHost));
+            for (size_t r = 0; r < nr; r++) std::memcpy(records + 12 * r, &h[kRecF4 * r], 3 * sizeof(float4));
+        }
     }
     *num_nodes = nn;
     *num_records = nr;

@@ -243,12 +243,12 @@ struct BvhBuildInput {
 };
 struct BvhBuildOutput {
     Bvh4Node *nodes4;   // device, collapsed 4-wide quantized tree
-    float4 *prims;      // device, 3 * n
+    float4 *prims;      // device, kRecF4 * num_records (record slots, pt_scene.h)
     float4 *attrs;      // device, kAttrStride * n shading records (same order)
     uint32_t root_link4;      // link of the root (internal 0 or a leaf)
     uint32_t num_nodes4;
     uint32_t depth4;    // levels of the BVH4 (1 = root only); 0 = not measured (A/B collapse)
-    uint32_t num_records = 0; // primitive records
+    uint32_t num_records = 0; // record slots (leaves on even slots; holes between)
     // first node of each BVH4 level (breadth-first collapse order) and the end; empty when
     // not measured.  Children always lie on a later level (bottom-up refits walk it backwards).
     std::vector<uint32_t> level_start;

@@ -390,7 +390,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     if (TL) {
                         bin = sc.instances[sc.prim_inst[best_idx]].bin;
                     } else {
-                        const uint32_t mt = __float_as_uint(sc.prims[3 * best_idx + 2].w);
+                        const uint32_t mt = __float_as_uint(sc.prims[kRecF4 * best_idx + 2].w);
                         bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
                     }
                 }

@@ -84,7 +84,8 @@ struct DevInstance {
     uint32_t bin;         // material bin of the instance's hits (0 miss, 1..7 EMatType, 8 unknown)
     float margin[2];      // object-space box margin: margin[0] * (|o| + t |d|) + margin[1]
     float wlo[3], whi[3];  // world box of the instance's world-space primitives
-    int32_t wrec_delta;    // world-space record of BLAS record i: wprims[3 * (i + wrec_delta)]
+    int32_t wrec_delta;    // world-space record of BLAS record slot i: wprims[kRecF4 * (i + wrec_delta)]
+    uint32_t rec_base;     // the shape's first BLAS record slot (two-level; attr_base counts primitives)
     // world-space copy of the shape's BLAS (two-level "world" mode): object nodes
     // [obj_nbase, obj_nbase + obj_ncount) -> world nodes from wnode_base
     uint32_t obj_nbase, obj_ncount, wnode_base;
@@ -123,6 +124,13 @@ PT_HD uint32_t leaf_first(int link) { return ((uint32_t)~link) >> 3; }
 PT_HD uint32_t leaf_count(int link) { return (((uint32_t)~link) & 7u) + 1u; }
 
 constexpr uint32_t kPrimSphereBit = 0x80000000u;
+// Primitive records: 4 float4 = 64 B per record slot (v0 | global id + sphere bit, v1 |
+// instance, v2 | material bin, unused), and every leaf starts on an even slot, i.e. on a
+// 128-B L2 line: a two-primitive leaf is one line instead of 96 B straddling up to two.  A
+// leaf of c primitives takes 2 ceil(c / 2) slots; unused slots are holes (all bits set).
+constexpr uint32_t kRecF4 = 4;
+constexpr uint32_t kRecHole = 0xFFFFFFFFu;  // a.w and b.w of a hole slot
+PT_HD uint32_t leaf_slots(uint32_t count) { return (count + 1u) & ~1u; }
 constexpr uint32_t kAttrStride = 8;  // float4 per shading record (one 128-B line)
 
 struct Camera {
@@ -132,7 +140,7 @@ struct Camera {
 
 struct DeviceScene {
     const Bvh4Node *nodes4;
-    const float4 *prims;  // 3 float4 per primitive, Morton order
+    const float4 *prims;  // kRecF4 float4 per record slot, leaf order (holes between leaves)
     const float4 *attrs;  // kAttrStride float4 per primitive, same order (hit reconstruction)
     uint32_t num_prims;
     uint32_t root_link4;  // link of the root (internal 0 or a leaf), kTraverseDone = empty

@@ -31,9 +31,9 @@ __device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const 
     const uint32_t first = leaf_first(leaf);
     const uint32_t count = leaf_count(leaf);
     for (uint32_t i = first; i < first + count; i++) {
-        const float4 a = sc.prims[3 * i + 0];
-        const float4 b = sc.prims[3 * i + 1];
-        const float4 c = sc.prims[3 * i + 2];
+        const float4 a = sc.prims[kRecF4 * i + 0];
+        const float4 b = sc.prims[kRecF4 * i + 1];
+        const float4 c = sc.prims[kRecF4 * i + 2];
         // the whole 48-B record in one round trip: without this the compiler sinks the
         // vertex loads below the sphere-bit branch, a second dependent fetch per record
         asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(c.x),
@@ -78,13 +78,13 @@ __device__ __forceinline__ bool intersect_leaf_tl(const DeviceScene &sc, const R
                                                   bool any) {
     // the instance's world-space records (fl(to_world * v), precomputed per instance):
     // no per-triangle transform in the loop
-    const float4 *rec = sc.wprims + 3 * (int64_t)sc.instances[inst].wrec_delta;
+    const float4 *rec = sc.wprims + kRecF4 * (int64_t)sc.instances[inst].wrec_delta;
     const uint32_t first = leaf_first(leaf);
     const uint32_t count = leaf_count(leaf);
     for (uint32_t i = first; i < first + count; i++) {
-        const float4 a = rec[3 * i + 0];
-        const float4 b = rec[3 * i + 1];
-        const float4 c = rec[3 * i + 2];
+        const float4 a = rec[kRecF4 * i + 0];
+        const float4 b = rec[kRecF4 * i + 1];
+        const float4 c = rec[kRecF4 * i + 2];
         const uint32_t key = __float_as_uint(a.w);
         if (STATS) prims_tested++;
         float t, b1 = 0.f, b2 = 0.f;

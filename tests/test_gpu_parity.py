@@ -932,7 +932,12 @@ def test_cpu_oracle_on_the_engine_bvh4_arrays():
     gpu = pt.buffers.get("pt accum buffer").cpu().numpy()
     nodes, recs, root = pt.export_bvh4()
     pt.close_engine()
-    assert len(nodes) > 1 and len(recs) == oracle.OracleScene(desc).num_prims and root == 0
+    # record slots: every primitive exactly once, holes between leaves (pt_scene.h kRecF4)
+    ids = np.ascontiguousarray(recs).view(np.uint32).reshape(len(recs), -1)[:, 3]
+    live = ids != 0xFFFFFFFF
+    n_prims = oracle.OracleScene(desc).num_prims
+    assert len(nodes) > 1 and root == 0 and len(recs) >= n_prims
+    assert np.array_equal(np.sort(ids[live] & 0x7FFFFFFF), np.arange(n_prims, dtype=np.uint32))
     own = oracle.OracleScene(desc)
     q4 = oracle.OracleScene(desc)
     q4.use_bvh4(nodes, recs, root)
