@@ -1,11 +1,12 @@
 #!/bin/bash
-# r04 final evidence on one box: GPU suite + smoke; config-4 PMC passes of this build (per-ray
-# VALU / HBM bytes the bench's roofline reads, copied into profiles/ before the bench); the
-# default bench (CPU baseline, timed-frame and drop-in checks); config 5; a same-box A/B against
-# the r03 library; the OnRun shard probe; rocprofv3 kernel stats and the timed-launch check.
+# r04 final evidence on one box: GPU suite + smoke; config-4 and config-5 PMC passes of this
+# build (per-ray VALU / HBM bytes the bench's roofline reads, copied into profiles/ before the
+# benches); the default bench (CPU baseline, timed-frame and drop-in checks); config 5; a same-box
+# A/B against the r03 library; the OnRun shard probe; rocprofv3 kernel stats and the timed-launch
+# check.
 set -u
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r04f2
+O=$R/gpurun_out/r04f3
 mkdir -p $O
 export TMPDIR=/tmp
 cd $R
@@ -18,6 +19,11 @@ cd $R
 cp gpurun_out/pmc_config4.json $O/pmc_config4.json && cp gpurun_out/pmc_config4.json profiles/pmc_config4.json
 mv gpurun_out/pmc_summary.txt $O/pmc_summary4.txt; rm -rf gpurun_out/pmc
 python3 -c "import json; d=json.load(open('$O/pmc_config4.json')); print('pmc4', round(d['traffic_bytes_per_ray'],1), 'B/ray', round(d['valu_insts_per_ray'],2), 'VALU/ray')"
+CONFIG=5 PUPIL_ROUND=r04 bash tools/gpu_pmc.sh > $O/pmc5.log 2>&1 || { tail -5 $O/pmc5.log; exit 1; }
+cd $R
+cp gpurun_out/pmc_config5.json $O/pmc_config5.json && cp gpurun_out/pmc_config5.json profiles/pmc_config5.json
+mv gpurun_out/pmc_summary.txt $O/pmc_summary5.txt; rm -rf gpurun_out/pmc
+python3 -c "import json; d=json.load(open('$O/pmc_config5.json')); print('pmc5', round(d['traffic_bytes_per_ray'],1), 'B/ray', round(d['valu_insts_per_ray'],2), 'VALU/ray')"
 timeout -k 10 500 python bench.py > $O/bench4.log 2>&1 || { tail -5 $O/bench4.log; exit 1; }
 grep '^{' $O/bench4.log | tail -1 > $O/bench4.json; cut -c1-300 $O/bench4.json
 timeout -k 10 900 python bench.py --config 5 --steps 3 --warmup 6 > $O/bench5.log 2>&1 || { tail -5 $O/bench5.log; exit 1; }
