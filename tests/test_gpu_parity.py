@@ -951,6 +951,48 @@ def test_cpu_oracle_on_the_engine_bvh4_arrays():
     assert np.array_equal(q4.closest(rays).view(np.uint32), own.closest(rays).view(np.uint32))
 
 
+@pytest.mark.parametrize("leaf_size", [1, 2, 3])
+def test_record_slots_put_every_leaf_on_one_line(leaf_size):
+    """Record slots (pt_scene.h kRecF4): every leaf link names an even slot (a 128-B line),
+    a leaf of c primitives owns 2 ceil(c/2) slots, no slot belongs to two leaves, every
+    primitive sits in exactly one leaf slot and no leaf names a hole; the frame stays equal
+    to the oracle's at each leaf size.  Runs in a subprocess (PUPIL_LEAF_SIZE is read once)."""
+    import subprocess
+    import sys
+    code = f"""
+import numpy as np, torch, oracle
+from pupiloptixlab_amd import scenes
+from pupiloptixlab_amd.pt_pass import PTPass
+desc = scenes.sphere_field(9, 64, 48, 3, seed=7).desc()
+pt = PTPass(device=0); pt.set_scene(desc); pt.dirty = False
+pt.render(1); torch.cuda.synchronize()
+gpu = pt.buffers.get("pt accum buffer").cpu().numpy()
+nodes, recs, root = pt.export_bvh4(); pt.close_engine()
+links = np.ascontiguousarray(nodes).view(np.int32).reshape(len(nodes), 16)[:, 4:8].ravel()
+leaves = [int(l) for l in links if l < 0] + ([root] if root < 0 else [])
+ids = np.ascontiguousarray(recs).view(np.uint32).reshape(len(recs), 12)[:, 3]
+owner = np.full(len(recs), -1)
+for l in leaves:
+    v = (~l) & 0xFFFFFFFF
+    first, count = v >> 3, (v & 7) + 1
+    assert first % 2 == 0 and count <= {leaf_size}
+    span = (count + 1) & ~1
+    assert (owner[first:first + span] < 0).all()
+    owner[first:first + span] = l
+    assert (ids[first:first + count] != 0xFFFFFFFF).all()
+    assert (ids[first + count:first + span] == 0xFFFFFFFF).all()
+n = oracle.OracleScene(desc).num_prims
+assert np.array_equal(np.sort(ids[ids != 0xFFFFFFFF] & 0x7FFFFFFF), np.arange(n, dtype=np.uint32))
+ref = oracle.OracleScene(desc).render(spp=1)
+assert np.array_equal(gpu.view(np.uint32), ref["accum"].view(np.uint32))
+print("ok", len(recs), n)
+"""
+    env = dict(os.environ, PUPIL_LEAF_SIZE=str(leaf_size), PUPIL_ACCEL="flat")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
 def test_consecutive_launches_on_one_engine():
     """The persistent kernels reset their own dequeue heads and exit counters (the
     last wave out, pt_kernels.hip trace4_body): eight renders on ONE engine with
