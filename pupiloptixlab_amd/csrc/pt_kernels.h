@@ -161,6 +161,11 @@ __device__ __forceinline__ void st_ps(uint4 *a, uint4 v) {
 #define PUPIL_TRIM 1
 #endif
 
+// single-material scenes shade through k_shade_one<MAT> (A/B builds: -DPUPIL_SHADE_ONE_BUILD=0)
+#ifndef PUPIL_SHADE_ONE_BUILD
+#define PUPIL_SHADE_ONE_BUILD 1
+#endif
+
 // shade: a path that spawns no extension ray skips its dead thr / misc stores, and rad is
 // stored only when the hit added emission (A/B builds: -DPUPIL_SHADE_SKIP=0)
 #ifndef PUPIL_SHADE_SKIP

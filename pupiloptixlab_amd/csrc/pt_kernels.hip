@@ -912,6 +912,41 @@ __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))
     }
 }
 
+// Single-material scenes (DeviceScene::single_bin, list modes): the same launch with only the
+// miss path and material MAT compiled, so the register budget is that material's, not the
+// largest of the seven BSDFs' (126 VGPRs, 4 waves per SIMD): diffuse needs 101-105 and runs at
+// 5 waves (96 VGPRs, 7-10 spills; config 4 -2.8 % per step, profiles/r04_shade_one_ab.txt);
+// the other BSDFs spill 15-43 registers at 5 waves and stay at 4 (A/B: PUPIL_SHADE_ONE=0,
+// -DPUPIL_SHADE_DIFFUSE_WAVES).
+#ifndef PUPIL_SHADE_DIFFUSE_WAVES
+#define PUPIL_SHADE_DIFFUSE_WAVES 5
+#endif
+constexpr int shade_one_waves(uint32_t mat) { return mat == PUPIL_MAT_DIFFUSE ? PUPIL_SHADE_DIFFUSE_WAVES : 4; }
+template <int LIST, uint32_t MAT>
+__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(shade_one_waves(MAT)))) void k_shade_one(
+    DeviceScene sc, FrameParams fp, PathState ps, Queues q, uint32_t tag, uint32_t range_base, uint32_t range_n,
+    uint32_t fresh_range, uint32_t fresh_seed0) {
+    static_assert(LIST != kShadeBins, "single-material shading walks a list");
+    const uint32_t n_list = LIST == kShadeNext || LIST == kShadeNextRange ? q.counts[kCntNext] : 0u;
+    const uint32_t count = n_list + (LIST == kShadeAll || LIST == kShadeNextRange ? range_n : 0u);
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        const uint32_t p = i < n_list ? q.nxsh[i] : range_base + (i - n_list);
+        const bool miss = __float_as_uint(ld_ps(ps.hit + p).w) == kMissIndex;
+        const bool fresh = fresh_range && i >= n_list;
+        const uint32_t fresh_p = p - range_base;
+        uint32_t flags = 0;
+        if (miss) shade_miss(sc, fp, ps, p, fresh, fresh_p, fresh_seed0);
+        else flags = shade_hit<MAT>(sc, fp, ps, p, fresh, fresh_p, fresh_seed0);
+        if (fp.nee_count) {
+            const unsigned long long m = __ballot((flags & 4u) != 0u);
+            if (m && __lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_read_exec()) - 1)
+                atomicAdd(fp.nee_count, (unsigned long long)__popcll(m));
+        }
+        ps.sflags[p] = (uint8_t)((flags & 3u) | tag << 2);
+    }
+}
+
 // ------------------------------------------------------------------ accumulate
 __global__ __launch_bounds__(kShadeBlock) void k_accumulate(FrameParams fp, PathState ps, const float *aov_src,
                                                              uint32_t clear_flags) {
@@ -1069,6 +1104,31 @@ void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState 
     const uint32_t fr = fresh_range && list != kShadeBins ? 1u : 0u;
 #define SHADE(L) \
     hipLaunchKernelGGL(k_shade_all<L>, g, b, 0, s, sc, fp, ps, q, tag, range_base, range_n, fr, fresh_seed0)
+#define SHADE1(L, M) \
+    hipLaunchKernelGGL((k_shade_one<L, M>), g, b, 0, s, sc, fp, ps, q, tag, range_base, range_n, fr, fresh_seed0)
+#define SHADE1_ALL(L)                                                       \
+    switch (sc.single_bin) {                                                \
+    case PUPIL_MAT_DIFFUSE: SHADE1(L, PUPIL_MAT_DIFFUSE); break;             \
+    case PUPIL_MAT_DIELECTRIC: SHADE1(L, PUPIL_MAT_DIELECTRIC); break;       \
+    case PUPIL_MAT_ROUGH_DIELECTRIC: SHADE1(L, PUPIL_MAT_ROUGH_DIELECTRIC); break; \
+    case PUPIL_MAT_CONDUCTOR: SHADE1(L, PUPIL_MAT_CONDUCTOR); break;         \
+    case PUPIL_MAT_ROUGH_CONDUCTOR: SHADE1(L, PUPIL_MAT_ROUGH_CONDUCTOR); break; \
+    case PUPIL_MAT_PLASTIC: SHADE1(L, PUPIL_MAT_PLASTIC); break;             \
+    case PUPIL_MAT_ROUGH_PLASTIC: SHADE1(L, PUPIL_MAT_ROUGH_PLASTIC); break; \
+    default: SHADE1(L, 0u); break;                                          \
+    }
+    static const bool one = [] {
+        const char *e = std::getenv("PUPIL_SHADE_ONE");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (one && PUPIL_SHADE_ONE_BUILD && sc.single_bin && list != kShadeBins) {
+        switch (list) {
+        case kShadeAll: SHADE1_ALL(kShadeAll); break;
+        case kShadeNext: SHADE1_ALL(kShadeNext); break;
+        default: SHADE1_ALL(kShadeNextRange); break;
+        }
+        return;
+    }
     switch (list) {
     case kShadeAll: SHADE(kShadeAll); break;
     case kShadeNext: SHADE(kShadeNext); break;
@@ -1076,6 +1136,8 @@ void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState 
     default: SHADE(kShadeBins); break;
     }
 #undef SHADE
+#undef SHADE1
+#undef SHADE1_ALL
 }
 
 __global__ __launch_bounds__(256) void k_node_bound(const Bvh4Node *nodes, uint64_t n, uint32_t *out) {
