@@ -606,14 +606,20 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
                    (pt->pipe.empty() ||
                     pt->pipe.front().seed + pt->pipe.front().consumed * fp.spp == launch->random_seed));
     const uint32_t nl = fp.num_local;
-    if ((size_t)K * G * np > pt->cap) {  // growing the ring loses its contents
+    // a render that starts no frame ahead has none in flight either (speculation is off only
+    // right after a reset) and works on slot 0, frame 0: the ring is allocated for frames ahead
+    // only once a render speculates, so a camera moving every OnRun runs on the path-state
+    // footprint of PUPIL_AHEAD=0.  K and G stay as computed: the pipeline key does not change
+    // when speculation starts
+    const auto ring_need = [&]() { return speculate ? (size_t)K * G * np : (size_t)np; };
+    if (ring_need() > pt->cap) {  // growing the ring loses its contents
         reset = true;
         pt->pipe.clear();
-        int rc = ensure_state(pt, (size_t)K * G * np);
-        while (rc == PUPIL_ERR_OOM && K * G > 1) {  // a smaller ring, down to no frames ahead
+        int rc = ensure_state(pt, ring_need());
+        while (rc == PUPIL_ERR_OOM && speculate && K * G > 1) {  // a smaller ring, down to no frames ahead
             if (K > 1) K = K > 2 ? K / 2 : 1;
             else G = G > 2 ? G / 2 : 1;
-            rc = ensure_state(pt, (size_t)K * G * np);
+            rc = ensure_state(pt, ring_need());
         }
         if (rc) return rc;
         key[8] = G;
