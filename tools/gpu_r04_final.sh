@@ -6,7 +6,7 @@
 # check.
 set -u
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r04f4
+O=$R/gpurun_out/r04f5
 mkdir -p $O
 export TMPDIR=/tmp
 cd $R
