@@ -757,6 +757,10 @@ def test_moving_camera_cadence_starts_no_frames_ahead():
         c = pt.stats()
         assert c["frames_in_flight"] == 0, k
         assert c["rays_traced_total"] - t0 == c["primary_rays"] + c["extension_rays"] + c["shadow_rays"]
+        one_frame_ring = c["ring_bytes"]
+        if k == 0:
+            ring0 = one_frame_ring
+        assert one_frame_ring == ring0, k  # no render speculated: the ring holds one frame
         d = World().load_scene(scenes.cornell_xml(os.path.join(TMP, "cb48d5.xml"), 48, 48, 5)).desc()
         d.camera_to_world[:] = [float(x) for x in c2w]
         ref = oracle.OracleScene(d).render(spp=1)["accum"]
@@ -765,7 +769,9 @@ def test_moving_camera_cadence_starts_no_frames_ahead():
     for _ in range(3):  # the camera stops: the OnRuns continue each other and pipeline
         pt.render(1)
     torch.cuda.synchronize()
-    assert pt.stats()["frames_in_flight"] > 0
+    c = pt.stats()
+    assert c["frames_in_flight"] > 0
+    assert c["ring_bytes"] > ring0  # the first speculating render allocated the ring
     pt.close_engine()
 
 
