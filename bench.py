@@ -29,6 +29,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
+SPEC_CLOCK_GHZ = 2.4  # MI355X max engine clock, MI355X_MICROARCH.md chip table
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
@@ -461,6 +462,18 @@ def gather_ceiling(footprint_bytes):
     except (OSError, ValueError, IndexError, subprocess.SubprocessError):
         return None
 
+def simd_efficiency(st):
+    """Lane utilisation of the persistent traversal (counter frame, trace4_body's diagnostics):
+    the fraction of a wave's 64 lanes doing useful work per node-loop and leaf-loop iteration,
+    and the lanes each refill activates.  What the VALU-issue fraction hides: an issued wave
+    instruction with 24 active lanes costs the same 2 cycles as one with 64."""
+    if not st.get("node_loop_iters"):
+        return None
+    return {"node_loop": round(st["node_loop_lanes"] / (64.0 * st["node_loop_iters"]), 4),
+            "leaf_loop": round(st["leaf_loop_lanes"] / (64.0 * max(1, st["leaf_loop_iters"])), 4),
+            "lanes_per_refill": round(st["refill_lanes"] / max(1, st["refills"]), 2),
+            "node_loop_iters": int(st["node_loop_iters"]), "leaf_loop_iters": int(st["leaf_loop_iters"])}
+
 def roofline(args, st_bytes, timed):
     """st_bytes: the counter frame's stats (per-ray node visits, primitive tests, bytes);
     timed: this rank's timed steps -- summed traversal launch time (HIP events on the
@@ -505,7 +518,10 @@ def roofline(args, st_bytes, timed):
             cands["valu-issue"] = {"achieved": need / sec / 1e9, "peak": simds * pmc["clock_ghz"],
                                    "unit": "G SIMD-cycles/s",
                                    "how": "PMC SQ_INSTS_VALU per traced ray x rays per launch x 2 cycles (wave64 on "
-                                          "SIMD-32) over 1024 SIMDs at the GRBM-measured clock"}
+                                          "SIMD-32) over 1024 SIMDs at the GRBM-measured clock",
+                                   # the same issue rate against the 2.4 GHz spec clock (MI355X_MICROARCH.md)
+                                   "frac_at_spec_clock": round(need / sec / 1e9 / (simds * SPEC_CLOCK_GHZ), 4),
+                                   "valu_insts_per_ray": round(pmc["valu_insts_per_ray"], 2)}
     for c in cands.values():
         c["frac"] = round(c["achieved"] / c["peak"], 4)
         c["achieved"] = round(c["achieved"], 2)
@@ -518,6 +534,7 @@ def roofline(args, st_bytes, timed):
             v["note"] = ("above the uniform-random gather rate of a node-array-sized table: the traversal's fetches "
                          "are served with more locality than random gathers; not a ceiling")
     out = {"kernel": kernel, "ms_per_launch": round(ms, 4), "launches": int(launches),
+           "simd_efficiency": simd_efficiency(st_bytes),
            "rays_per_launch": round(rays_launch, 1), "traffic": round(traffic, 1) if traffic else None,
            # SURVEY.md §8(d) algorithmic bytes (32 B ray + 16 B hit + 64 B/node + 48 B/primitive): the BVH
            # is cache-resident (L2 + Infinity Cache), so these exceed what HBM delivers; not a fraction of HBM
@@ -529,6 +546,8 @@ def roofline(args, st_bytes, timed):
         b = cands[bound]
         out.update({"bound": bound, "achieved": b["achieved"], "peak": round(b["peak"], 2), "unit": b["unit"],
                     "frac": b["frac"]})
+        if "frac_at_spec_clock" in b:
+            out["frac_at_spec_clock"] = b["frac_at_spec_clock"]
     else:
         out.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None})
     keys = ["bound", "achieved", "peak", "unit", "frac", "traffic"]

@@ -6,7 +6,9 @@
 //
 // usage: pupil_path_tracer <scene.xml> [frames=16] [out.exr|.hdr|.pfm] [device=0]
 //        PUPIL_BENCH=warmup,frames,spp pupil_path_tracer <scene.xml>   (drop-in cadence benchmark)
+#include <algorithm>
 #include <chrono>
+#include <string>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -24,11 +26,21 @@
 // progressive render (accumulation restarts once, through a CameraChange event, as
 // when the user stops moving the camera).  `warmup` untimed and `frames` timed frames
 // (steady_clock around the loop); the rays are the engine's exact running total over
-// the timed OnRuns.  PUPIL_BENCH_ACCUM=<file>: the final "pt accum buffer" (rank 0,
+// the timed OnRuns.  Every timed OnRun is also timed on its own (steady_clock around
+// System::Run(1), whose OnRun ends in a stream synchronisation): the line reports the
+// p50 / p99 / max OnRun time -- with frame groups one OnRun in G carries the traversal of G
+// frames and the others only accumulate (System::Run -> FrameFinished shows each one,
+// system.cpp:95-101).  PUPIL_BENCH_ACCUM=<file>: the final "pt accum buffer" (rank 0,
 // raw float32 RGBA) for a bit-exact comparison with a batched render of the same
 // seeds.  PUPIL_BENCH_MOVING=1: the interactive cadence instead -- the camera moves
 // (CameraHelper::SetCameraToWorld, a CameraChange) before every OnRun, so every frame
 // restarts accumulation and no render continues the previous one.  Prints one JSON line.
+static double pct(std::vector<double> v, double q) {
+    if (v.empty()) return 0.0;
+    std::sort(v.begin(), v.end());
+    return v[std::min(v.size() - 1, (size_t)(q * (double)v.size()))];
+}
+
 static int Bench(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spec) {
     int warmup = 1, frames = 5, spp = 8;
     if (std::sscanf(spec, "%d,%d,%d", &warmup, &frames, &spp) != 3 || frames < 1 || spp < 1 || warmup < 0) {
@@ -42,23 +54,26 @@ static int Bench(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spe
     float s2c[16], c2w[16];
     w->camera->Snapshot(s2c, c2w);
     uint32_t step = 0;
+    std::vector<double> onrun_ms;
+    bool timed = false;
     auto frame = [&]() {
-        if (!moving) {
-            system.Run((uint32_t)spp);
-            return;
-        }
-        for (int j = 0; j < spp; j++) {  // a camera move before every OnRun
-            float c[16];
-            std::memcpy(c, c2w, sizeof(c));
-            c[3] += 1e-4f * (float)(++step);
-            w->camera->SetCameraToWorld(c);
+        for (int j = 0; j < spp; j++) {
+            if (moving) {  // a camera move before every OnRun
+                float c[16];
+                std::memcpy(c, c2w, sizeof(c));
+                c[3] += 1e-4f * (float)(++step);
+                w->camera->SetCameraToWorld(c);
+            }
+            const auto a = std::chrono::steady_clock::now();
             system.Run(1);
+            if (timed) onrun_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());
         }
     };
     for (int k = 0; k < warmup; k++) frame();
     if (hipDeviceSynchronize() != hipSuccess) return 1;
     pupil_pt_counters c0{}, c1{};
     if (!pass.Stats(c0)) return 1;
+    timed = true;
     const auto t0 = std::chrono::steady_clock::now();
     for (int k = 0; k < frames; k++) frame();
     if (hipDeviceSynchronize() != hipSuccess) return 1;
@@ -80,12 +95,60 @@ static int Bench(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spe
         }
         std::fclose(f);
     }
-    std::printf("{\"ms_per_frame\": %.4f, \"onrun_ms\": %.4f, \"mrays_per_s_rank0\": %.2f, \"rays_per_frame_rank0\": %.0f, "
+    std::printf("{\"ms_per_frame\": %.4f, \"onrun_ms\": %.4f, \"onrun_ms_p50\": %.4f, \"onrun_ms_p99\": %.4f, "
+                "\"onrun_ms_max\": %.4f, \"mrays_per_s_rank0\": %.2f, \"rays_per_frame_rank0\": %.0f, "
                 "\"frames\": %d, \"warmup\": %d, \"spp\": %d, \"ranks\": %d, \"frames_in_flight\": %llu, "
                 "\"moving_camera\": %s, \"ring_bytes\": %llu}\n",
-                1e3 * s / frames, 1e3 * s / (frames * spp), rays / s / 1e6, rays / frames, frames, warmup, spp,
-                g ? g->Info().world : 1, (unsigned long long)c1.frames_in_flight, moving ? "true" : "false",
-                (unsigned long long)c1.ring_bytes);
+                1e3 * s / frames, 1e3 * s / (frames * spp), pct(onrun_ms, 0.5), pct(onrun_ms, 0.99), pct(onrun_ms, 1.0),
+                rays / s / 1e6, rays / frames, frames, warmup, spp, g ? g->Info().world : 1,
+                (unsigned long long)c1.frames_in_flight, moving ? "true" : "false", (unsigned long long)c1.ring_bytes);
+    return 0;
+}
+
+// PUPIL_BENCH_WASTE="k1,k2,...": what speculation costs when the camera moves.  For each k: a
+// camera change, k static OnRuns (the engine pipelines frames ahead once the OnRuns continue
+// each other), then another camera change, which drops the frames in flight.  Prints the rays
+// traced over each static stretch (engine running totals) and the frames in flight that the
+// move dropped; the same run with PUPIL_AHEAD=0 traces exactly the displayed frames' rays, so
+// the difference of the two is the speculation the move discarded.
+static int BenchWaste(Pupil::System &system, Pupil::pt::PTPass &pass, const char *spec) {
+    std::vector<int> ks;
+    for (const char *p = spec; *p;) {
+        ks.push_back(std::atoi(p));
+        while (*p && *p != ',') p++;
+        if (*p == ',') p++;
+    }
+    Pupil::world::World *w = system.GetWorld();
+    float s2c[16], c2w[16];
+    w->camera->Snapshot(s2c, c2w);
+    uint32_t step = 0;
+    auto move = [&]() {
+        float c[16];
+        std::memcpy(c, c2w, sizeof(c));
+        c[3] += 1e-4f * (float)(++step);
+        w->camera->SetCameraToWorld(c);
+    };
+    std::string out = "{\"waste\": [";
+    for (size_t i = 0; i < ks.size(); i++) {
+        move();
+        pupil_pt_counters a{}, b{};
+        if (!pass.Stats(a)) return 1;
+        std::vector<double> ms;
+        for (int j = 0; j < ks[i]; j++) {
+            const auto t0 = std::chrono::steady_clock::now();
+            system.Run(1);
+            ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
+        if (hipDeviceSynchronize() != hipSuccess || !pass.Stats(b)) return 1;
+        char rec[256];
+        std::snprintf(rec, sizeof(rec), "%s{\"k\": %d, \"rays\": %llu, \"frames_dropped_by_move\": %llu, \"onrun_ms_max\": %.3f}",
+                      i ? ", " : "", ks[i], (unsigned long long)(b.rays_traced_total - a.rays_traced_total),
+                      (unsigned long long)b.frames_in_flight, pct(ms, 1.0));
+        out += rec;
+    }
+    move();
+    system.Run(1);  // the last stretch's frames in flight are dropped here
+    std::printf("%s]}\n", out.c_str());
     return 0;
 }
 
@@ -183,6 +246,8 @@ int main(int argc, char **argv) {
             rc = 1;
         } else if (const char *bench = std::getenv("PUPIL_BENCH")) {
             rc = Bench(*system, *pt_pass, bench);
+        } else if (const char *waste = std::getenv("PUPIL_BENCH_WASTE")) {
+            rc = BenchWaste(*system, *pt_pass, waste);
         } else if (const char *tt = std::getenv("PUPIL_THREAD_TEST")) {
             rc = ThreadTest(*system, *pt_pass, tt);
         } else {

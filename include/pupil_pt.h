@@ -233,7 +233,8 @@ typedef struct pupil_pt_counters {
     uint64_t bvh_nodes;
     uint64_t bvh_prims;
     double build_ms;
-    double last_render_ms;   /* device time of the last pupil_pt_render (events) */
+    double last_render_ms;   /* device time of the last pupil_pt_render (events), recorded only for
+                              * renders that set collect_stats or request stage times; 0 otherwise */
     double trace_ms;         /* device time of the traversal kernels in the last render (collect_stats
                               * bit 1), or in every PUPIL_STATS_TRACE_TIMING render since the last read */
     double trace_bytes;      /* algorithmic bytes of the traversal kernels (collect_stats) */
@@ -291,6 +292,16 @@ typedef struct pupil_pt_counters {
      * (the slab test's rounding bound is taken per ray from it) */
     float node_bound[3];
     uint32_t pad_counters;
+    /* ABI 5.  collect_stats, persistent traversal kernels: SIMD efficiency -- node-loop wave
+     * iterations and the lanes active in them, leaf-loop wave iterations and their active
+     * lanes, refills and the lanes they activated (active lanes / (64 x iterations) = the
+     * fraction of a wave's lanes doing useful work in that loop) */
+    uint64_t node_loop_iters;
+    uint64_t node_loop_lanes;
+    uint64_t leaf_loop_iters;
+    uint64_t leaf_loop_lanes;
+    uint64_t refills;
+    uint64_t refill_lanes;
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;
@@ -314,7 +325,9 @@ int pupil_pt_update_instances(pupil_pt *pt, uint32_t n, const uint32_t *ids, con
  * rewritten in place on the engine's stream when their shapes are unchanged */
 int pupil_pt_update_emitters(pupil_pt *pt, const pupil_scene_desc *scene);
 /* Asynchronous on hip_stream (a hipStream_t; NULL = the default null stream): the
- * output buffers are complete once work later enqueued on that stream runs. */
+ * output buffers are complete once work later enqueued on that stream runs.  Exception:
+ * with max_depth > 64 the call synchronises hip_stream every 16 bounces to read the list
+ * lengths back and stops once no path is left. */
 int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_launch *launch, void *hip_stream);
 int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out);
 int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank,

@@ -93,7 +93,10 @@ class Counters(C.Structure):
                 ("pipeline_slots", C.c_uint64), ("tlas_sah_splits", C.c_uint64),
                 ("queue_handed", C.c_uint64), ("queue_activated", C.c_uint64), ("queue_retired", C.c_uint64),
                 ("queue_listed", C.c_uint64), ("ring_bytes", C.c_uint64), ("ring_budget_bytes", C.c_uint64),
-                ("accel_refits", C.c_uint64), ("node_bound", C.c_float * 3), ("pad_counters", C.c_uint32)]
+                ("accel_refits", C.c_uint64), ("node_bound", C.c_float * 3), ("pad_counters", C.c_uint32),
+                # ABI 5
+                ("node_loop_iters", C.c_uint64), ("node_loop_lanes", C.c_uint64), ("leaf_loop_iters", C.c_uint64),
+                ("leaf_loop_lanes", C.c_uint64), ("refills", C.c_uint64), ("refill_lanes", C.c_uint64)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_ if name != "pad_counters"}

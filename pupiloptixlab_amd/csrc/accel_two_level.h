@@ -60,7 +60,10 @@ PT_HD int rebase_link(int link, uint32_t node_base, uint32_t prim_base) {
 
 // Builds the BLASes, fills the two-level fields of every instance (host copy
 // `insts`, uploaded to d_insts), their world boxes and the TLAS.
-// inst_shape[i] = shape index of instance i (ignored for spheres).
+// inst_shape[i] = shape index of instance i (ignored for spheres).  Returns 0, -1 on a HIP
+// error, -3 when the TLAS + BLAS depth exceeds the traversal stacks, -4 when the BLAS record
+// slots or instances exceed the 28-bit leaf links (accel_limits.h; past the world-mode limit
+// alone the build falls back to object mode instead).
 int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<uint32_t> &inst_shape,
                     std::vector<DevInstance> &insts, DevInstance *d_insts, const DevMaterial *d_mats,
                     uint32_t leaf_size, hipStream_t s, TwoLevelAccel &acc);

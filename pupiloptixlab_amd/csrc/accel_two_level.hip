@@ -27,6 +27,7 @@
 #include <numeric>
 #include <vector>
 
+#include "accel_limits.h"
 #include "accel_two_level.h"
 #include "bvh4_quant.h"
 
@@ -697,6 +698,7 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     std::vector<uint32_t> node_base(shapes.size(), 0), prim_base(shapes.size(), 0), rec_base(shapes.size(), 0);
     acc.tlas_cap = std::max(1u, n);
     uint32_t total_nodes = acc.tlas_cap, total_prims = 0, total_slots = 0, max_faces = 1;
+    uint64_t nodes64 = acc.tlas_cap, slots64 = 0;  // the same sums without wrap-around
     for (size_t k = 0; k < shapes.size(); k++)
         if (used[k]) max_faces = std::max(max_faces, shapes[k].num_faces);
     uint32_t *zeros = nullptr;
@@ -740,6 +742,15 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         total_nodes += blas[k].num_nodes4;
         total_prims += sh.num_faces;
         total_slots += sh.num_faces ? blas[k].num_records : 0u;
+        nodes64 += blas[k].num_nodes4;
+        slots64 += sh.num_faces ? blas[k].num_records : 0u;
+    }
+    // object-space BLAS leaf links name record slots in 28 bits, object-mode TLAS leaves an
+    // instance id (accel_limits.h); both structures need the object BLASes
+    if (!rc && (nodes64 > kMaxNodes4 || two_level_fit(slots64, 0, 0, n, false) == TwoLevelFit::None)) {
+        std::fprintf(stderr, "[pupil] two-level: %llu BLAS record slots / %llu nodes / %u instances exceed the link limits\n",
+                     (unsigned long long)slots64, (unsigned long long)nodes64, n);
+        rc = -4;
     }
     if (!rc && (hipMalloc((void **)&acc.nodes4, sizeof(Bvh4Node) * total_nodes) != hipSuccess ||
                 hipMalloc((void **)&acc.prims, sizeof(float4) * kRecF4 * (size_t)std::max(1u, total_slots)) != hipSuccess ||
@@ -824,6 +835,13 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
         verts[i] = shapes[k].num_vertices;
         faces[i] = slots;  // the BLAS record slots k_world_records copies
         instance_margin(d, shapes[k].vmax);
+    }
+    // world-mode leaf links name world record slots (the meshes' copies, then one 2-slot leaf
+    // per sphere) in 28 bits: beyond that the object-space structure serves the scene
+    if (acc.world && two_level_fit(slots64, wbase, spheres, n, true) != TwoLevelFit::World) {
+        std::fprintf(stderr, "[pupil] two-level: %llu world record slots + %llu spheres exceed the 28-bit leaf links, object mode\n",
+                     (unsigned long long)wbase, (unsigned long long)spheres);
+        acc.world = false;
     }
     int trc = 0;
     if (wbase >= (1ull << 31) ||

@@ -612,6 +612,9 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
     // footprint of PUPIL_AHEAD=0.  K and G stay as computed: the pipeline key does not change
     // when speculation starts
     const auto ring_need = [&]() { return speculate ? (size_t)K * G * np : (size_t)np; };
+    // a reset caused only by growing the ring (this render continues the last one) keeps the
+    // run count, so the render after the first speculating one speculates as well
+    const bool continued = !reset;
     if (ring_need() > pt->cap) {  // growing the ring loses its contents
         reset = true;
         pt->pipe.clear();
@@ -625,7 +628,10 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         key[8] = G;
     }
     const size_t cap_paths = (size_t)G * np;  // paths per ring slot
-    if (K * G > 1 && (size_t)K * G * 7 * nl > pt->aov_cap) {
+    // AOV scratch holds the AOVs of frames shaded ahead of their render: needed only once a
+    // render speculates (frames in flight imply an earlier speculating render allocated it), so a
+    // moving camera keeps the footprint of PUPIL_AHEAD=0 here too
+    if (speculate && K * G > 1 && (size_t)K * G * 7 * nl > pt->aov_cap) {
         reset = true;
         if (pt->aov_scratch) (void)hipFree(pt->aov_scratch);
         pt->aov_scratch = nullptr;
@@ -649,7 +655,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
             pt->ring_fresh = false;
         }
         pt->pipe.clear();
-        pt->pipe_run = 0;
+        pt->pipe_run = continued ? pt->pipe_run + 1 : 0;
         pt->pipe_slots = K;
         pt->pipe_np = np;
         pt->pipe_cap = cap_paths;
@@ -775,7 +781,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
 extern "C" {
 
 const char *pupil_last_error(void) { return g_last_error.c_str(); }
-int pupil_abi_version(void) { return 4; }
+int pupil_abi_version(void) { return 5; }
 
 int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank, uint32_t tile_world,
                           uint32_t *out_pixels, uint32_t *inout_count) {
@@ -951,6 +957,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
             }
             const int trc = build_two_level(tls, inst_shape, insts, d_insts, d_mats, pt->leaf_size, pt->own_stream, pt->tl);
             if (trc == -3) return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "TLAS + BLAS deeper than the traversal stacks hold"));
+            if (trc == -4) return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "two-level record slots beyond the 28-bit leaf links"));
             if (trc != 0) return cleanup(fail(PUPIL_ERR_HIP, "two-level acceleration build failed"));
             pt->build_ms = pt->tl.build_ms;
         } else {
@@ -1381,6 +1388,12 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
                              100.0 * (double)d[3] / (64.0 * (double)std::max(1ull, d[2])), d[4],
                              (double)d[5] / (double)std::max(1ull, d[4]));
             }
+            c.node_loop_iters = tc[2];  // trace4_body dg[0..5]
+            c.node_loop_lanes = tc[3];
+            c.leaf_loop_iters = tc[4];
+            c.leaf_loop_lanes = tc[5];
+            c.refills = tc[6];
+            c.refill_lanes = tc[7];
             c.node_visits = tc[0] + tc[14];
             c.prim_tests = tc[1] + tc[15];
             c.shadow_rays_reference = tc[16];

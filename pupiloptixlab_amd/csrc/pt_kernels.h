@@ -11,10 +11,7 @@
 namespace pupil {
 
 constexpr int kTraceBlock = 128;
-#ifndef PUPIL_W4_WAVES  // A/B builds only
-#define PUPIL_W4_WAVES 7
-#endif
-constexpr int kTraceWavesPerSimd = PUPIL_W4_WAVES;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8 waves at <= 64 VGPRs: 11 % slower, r03 A/B)
+constexpr int kTraceWavesPerSimd = 7;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8 waves at <= 64 VGPRs: 11 % slower, r03 A/B)
 constexpr int kTraceWavesPerSimdTL = 5;  // two-level variant (<= 96 VGPRs; A/B r02 on config 5: 4 waves 688, 5: 743, 6: 716 Mrays/s)
 constexpr int kStackOvf = 160;  // per-thread global overflow entries
 constexpr int kRing = 16;       // persistent BVH4 kernels: per-lane LDS ring entries (spills to the overflow column)
@@ -110,67 +107,28 @@ struct FrameParams {
     uint32_t aov_frame_stride;
 };
 
-// Path-state records are streamed with non-temporal loads / stores (PUPIL_NT, A/B builds: 0),
-// so the GBs of path state a step moves do not push BVH nodes and primitive records out of
+// Path-state records are streamed with non-temporal loads / stores (r03), so the GBs of path state a step moves do not push BVH nodes and primitive records out of
 // the L2s and the Infinity Cache.
-#ifndef PUPIL_NT
-#define PUPIL_NT 1
-#endif
 __device__ __forceinline__ float4 ld_ps(const float4 *a) {
-#if PUPIL_NT
     typedef float v4f __attribute__((ext_vector_type(4)));
     const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(a));
     return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *a;
-#endif
 }
 __device__ __forceinline__ uint4 ld_ps(const uint4 *a) {
-#if PUPIL_NT
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
     const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(a));
     return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return *a;
-#endif
 }
 __device__ __forceinline__ void st_ps(float4 *a, float4 v) {
-#if PUPIL_NT
     typedef float v4f __attribute__((ext_vector_type(4)));
     v4f w = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(w, reinterpret_cast<v4f *>(a));
-#else
-    *a = v;
-#endif
 }
 __device__ __forceinline__ void st_ps(uint4 *a, uint4 v) {
-#if PUPIL_NT
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
     v4u w = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(a));
-#else
-    *a = v;
-#endif
 }
-
-// persistent traversal: the path id, the best hit's record index and barycentrics in LDS, the
-// ray direction reloaded where needed, the overflow column recomputed on a spill (r04: 2 / 1
-// VGPR spills instead of 4 / 5, -1.8 % per launch, profiles/r04_trim_state_ab.txt; A/B
-// builds: -DPUPIL_TRIM=0)
-#ifndef PUPIL_TRIM
-#define PUPIL_TRIM 1
-#endif
-
-// single-material scenes shade through k_shade_one<MAT> (A/B builds: -DPUPIL_SHADE_ONE_BUILD=0)
-#ifndef PUPIL_SHADE_ONE_BUILD
-#define PUPIL_SHADE_ONE_BUILD 1
-#endif
-
-// shade: a path that spawns no extension ray skips its dead thr / misc stores, and rad is
-// stored only when the hit added emission (A/B builds: -DPUPIL_SHADE_SKIP=0)
-#ifndef PUPIL_SHADE_SKIP
-#define PUPIL_SHADE_SKIP 1
-#endif
 
 struct TraceStats {
     unsigned long long *counters;  // [0..1] closest-hit nodes/prims, [14..15] shadow, [2..13] diagnostics,

@@ -12,6 +12,7 @@
 #pragma once
 
 #include "../../include/pupil_pt.h"
+#include "accel_limits.h"
 #include "pt_math.h"
 
 namespace pupil {
@@ -116,12 +117,7 @@ constexpr int kTraverseDone = 0x76543210;
 // the lane to the TLAS (a positive link above kTraverseDone, never a node index).
 constexpr int kReturnLink = 0x7654321F;
 
-// Child link encoding: link >= 0 -> internal node index; link < 0 -> leaf,
-// ~link = (first_prim << 3) | (count - 1), count in [1, 8].
-constexpr int kLeafMax = 8;
-PT_HD int make_leaf(uint32_t first, uint32_t count) { return ~(int)((first << 3) | (count - 1)); }
-PT_HD uint32_t leaf_first(int link) { return ((uint32_t)~link) >> 3; }
-PT_HD uint32_t leaf_count(int link) { return (((uint32_t)~link) & 7u) + 1u; }
+// Child link encoding (make_leaf / leaf_first / leaf_count) and its 28-bit limit: accel_limits.h.
 
 constexpr uint32_t kPrimSphereBit = 0x80000000u;
 // Primitive records: 4 float4 = 64 B per record slot (v0 | global id + sphere bit, v1 |

@@ -22,7 +22,7 @@ __device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, 
 // Leaf intersection (flattened BVH4 and two-level world mode).  any = terminate on the first
 // hit (shadow ray); a compile-time constant except in the mixed persistent kernel.
 // dirf(): the ray direction, for sphere records only (the traversal may reload it instead of
-// keeping it live, PUPIL_TRIM)
+// keeping it live)
 template <bool STATS, typename DirF>
 __device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
                                                    float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
@@ -135,7 +135,6 @@ static_assert((kRing & (kRing - 1)) == 0, "ring size must be a power of two");
 
 struct RingStack {
     int *lds;  // this lane's column (stride kTraceBlock)
-#if PUPIL_TRIM
     // the overflow column is found from the block's base and the lane's LDS column only
     // when the ring spills or refills (no 64-bit per-lane pointer held across the loop)
     int *ovf_blk;       // this block's first overflow column (uniform)
@@ -145,10 +144,6 @@ struct RingStack {
         asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"((uint32_t)(lds - lds0)));  // not hoisted out of the loop
         return ovf_blk + lane;
     }
-#else
-    int *ovf;  // this lane's overflow column (stride ovf_stride)
-    __device__ __forceinline__ int *ovf_col() { return ovf; }
-#endif
     uint32_t ovf_stride;
     int sp;   // logical entries [0, sp)
     int bot;  // entries [0, bot) live in ovf, [bot, sp) in the ring
@@ -183,13 +178,9 @@ struct RingStack {
     }
 };
 
-// Child order of a BVH4 visit (A/B, PUPIL_SORT at build time): 5 = full sort (the
-// nearest child is descended, the others pushed far to near); 4 = nearest first and
-// farthest pushed first, the middle two unordered; 3 = nearest first only.  Only the
-// traversal order changes: hits are resolved by the (t, id) total order either way.
-#ifndef PUPIL_SORT
-#define PUPIL_SORT 5
-#endif
+// Child order of a BVH4 visit: the nearest child is descended, the others pushed far to
+// near (r03: partial sorts with 4 or 3 comparators were no faster).  Only the traversal
+// order depends on it: hits are resolved by the (t, id) total order either way.
 
 // Branch-free compare-exchange (selects, no divergent swap blocks).
 __device__ __forceinline__ void csel(float &ta, int &la, float &tb, int &lb) {
@@ -289,12 +280,8 @@ __device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, v
     csel(t[0], l[0], t[1], l[1]);
     csel(t[2], l[2], t[3], l[3]);
     csel(t[0], l[0], t[2], l[2]);
-#if PUPIL_SORT >= 4
     csel(t[1], l[1], t[3], l[3]);
-#endif
-#if PUPIL_SORT >= 5
     csel(t[1], l[1], t[2], l[2]);
-#endif
 }
 
 // Node fetch by a 32-bit byte offset from the uniform base (the engine keeps node

@@ -33,16 +33,20 @@ struct DistInfo {
 // RANK / WORLD_SIZE / LOCAL_RANK (torchrun's variables); world = 1 without them.
 DistInfo DistFromEnv() noexcept;
 
-// Identity of this launch, the same on every rank of it: the launcher's pid
-// (getppid: torchrun's agent, mpirun, a slurm step), TORCHELASTIC_RUN_ID /
-// _RESTART_COUNT, MASTER_PORT and WORLD_SIZE (PUPIL_RCCL_NONCE overrides it).
+// Identity of this launch, the same on every rank of it however each rank was started:
+// launch-wide environment only (MASTER_ADDR / MASTER_PORT, WORLD_SIZE,
+// TORCHELASTIC_RUN_ID / _RESTART_COUNT, SLURM_JOB_ID / _STEP_ID); PUPIL_RCCL_NONCE
+// overrides it.
 std::string DistLaunchNonce() noexcept;
 // Node-local file through which rank 0 hands its ncclUniqueId to the other ranks:
 // PUPIL_RCCL_ID_FILE, else /tmp/pupil_rccl_<MASTER_PORT>_<hash of the nonce>.id.
 std::string DistIdPath() noexcept;
-// The id file: magic, the launch nonce, the id.  Write removes any previous file first
-// and renames a complete temporary into place.  Read returns 1 (id of this launch),
-// 0 (absent or incomplete) or -1 (left by another launch: never used).
+// The id file: magic, the launch nonce, the writer (host name, pid and the process start
+// time in clock ticks since boot, /proc/<pid>/stat field 22), the id.  Write removes any
+// previous file first and renames a complete temporary into place.  Read returns 1 (id of
+// this launch), 0 (absent or incomplete) or -1 (never used: another launch's nonce, or a
+// writer on this host that is no longer running -- a crashed or finished earlier launch
+// with the same environment).  No wall clock is compared, so ranks may start any time apart.
 bool WriteIdFile(const std::string &path, const std::string &nonce, const void *id, size_t size) noexcept;
 int ReadIdFile(const std::string &path, const std::string &nonce, void *id, size_t size) noexcept;
 
@@ -57,6 +61,12 @@ public:
     // the others through `id_path` (a file on the node's local filesystem, written
     // atomically); every rank then joins the communicator on `device`.
     bool Init(const DistInfo &d, int device, const std::string &id_path) noexcept;
+    // PUPIL_GATHER_TRANSPORT=host (tests only, never the default): no RCCL communicator;
+    // every rank stages its compact tiles through pinned host memory and a file in a
+    // per-launch directory (DistIdPath() + ".d"), which rank 0 reads back.  It lets N rank
+    // processes share ONE GPU (RCCL refuses two ranks on one device), so the rank != 0 paths
+    // of Gather and PTPass::SetScene run on a single-GPU box; the frames are bit-identical
+    // to the RCCL transport's (the same bytes move).
     // Per frame size: the tile maps of every rank (rank 0 keeps them on the device).
     bool Setup(uint32_t width, uint32_t height) noexcept;
     // Gathers every rank's compact float4 buffer (this rank's `LocalPixels()` pixels,
@@ -73,6 +83,13 @@ private:
     std::vector<uint32_t> m_counts;   // pixels per rank
     std::vector<uint32_t *> m_maps;   // rank 0: device pixel map per rank
     std::vector<float *> m_staging;   // rank 0: received compact buffers per rank
+    // host transport (tests): exchange directory, frames gathered so far, pinned staging
+    bool m_host = false;
+    std::string m_dir;
+    uint64_t m_frame = 0;
+    std::vector<float *> m_pinned;    // rank 0: one per rank; others: their own tiles
+    bool GatherHost(const void *local, hipStream_t stream) noexcept;
+    bool Scatter(const void *local, void *full, hipStream_t stream) noexcept;
     void Release() noexcept;
 };
 

@@ -7,6 +7,8 @@
 #include <cstring>
 #include <thread>
 
+#include <cerrno>
+
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -22,18 +24,43 @@ int env_int(const char *name, int def) {
     return v && *v ? std::atoi(v) : def;
 }
 
-constexpr char kIdMagic[8] = {'P', 'U', 'P', 'I', 'L', 'I', 'D', '1'};
+constexpr char kIdMagic[8] = {'P', 'U', 'P', 'I', 'L', 'I', 'D', '2'};
 
-// wall clock when this library was loaded (about when the rank process started): an id
-// file written before it, less a launcher skew allowance, belongs to an earlier launch
-const auto g_loaded = std::chrono::system_clock::now();
-constexpr int kLaunchSkewSeconds = 30;
+// start time of process `pid` in clock ticks since boot (/proc/<pid>/stat field 22), 0 when
+// it does not exist: (pid, start time) names one process for the lifetime of the host
+uint64_t proc_start_ticks(long pid) {
+    char path[64];
+    std::snprintf(path, sizeof(path), "/proc/%ld/stat", pid);
+    FILE *f = std::fopen(path, "r");
+    if (!f) return 0;
+    char buf[1024];
+    const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+    std::fclose(f);
+    buf[n] = '\0';
+    const char *p = std::strrchr(buf, ')');  // the command name may hold spaces and parentheses
+    if (!p) return 0;
+    unsigned long long v = 0;
+    // fields 3..21 after the name, then 22 = starttime
+    if (std::sscanf(p + 2, "%*c %*d %*d %*d %*d %*d %*u %*u %*u %*u %*u %*u %*u %*d %*d %*d %*d %*d %*d %llu", &v) != 1)
+        return 0;
+    return v;
+}
 
-bool older_than_this_launch(const std::string &path) {
-    struct stat st;
-    if (stat(path.c_str(), &st) != 0) return false;
-    const auto loaded = std::chrono::duration_cast<std::chrono::seconds>(g_loaded.time_since_epoch()).count();
-    return (long long)st.st_mtime < (long long)loaded - kLaunchSkewSeconds;
+std::string host_name() {
+    char h[256] = {0};
+    if (gethostname(h, sizeof(h) - 1) != 0) return "?";
+    return h;
+}
+
+bool write_str(FILE *f, const std::string &s) {
+    const uint32_t n = (uint32_t)s.size();
+    return std::fwrite(&n, sizeof(n), 1, f) == 1 && (n == 0 || std::fwrite(s.data(), n, 1, f) == 1);
+}
+bool read_str(FILE *f, std::string &s, uint32_t max) {
+    uint32_t n = 0;
+    if (std::fread(&n, sizeof(n), 1, f) != 1 || n > max) return false;
+    s.assign(n, '\0');
+    return n == 0 || std::fread(s.data(), n, 1, f) == 1;
 }
 
 // rank 0 -> the others: the 128-byte ncclUniqueId through a file, renamed into place.
@@ -49,9 +76,7 @@ bool exchange_id(const DistInfo &d, const std::string &path, ncclUniqueId &id) {
     const auto t0 = std::chrono::steady_clock::now();
     bool warned = false;
     for (;;) {
-        // an id written before this launch began (a crashed run with the same launch
-        // environment) is skipped like one of another launch
-        const int r = older_than_this_launch(path) ? -1 : ReadIdFile(path, nonce, &id, sizeof(id));
+        const int r = ReadIdFile(path, nonce, &id, sizeof(id));
         if (r > 0) return true;
         if (r < 0 && !warned) {
             Log("rank %d: ignoring %s, left by another launch (waiting for rank 0)", d.rank, path.c_str());
@@ -103,9 +128,11 @@ bool WriteIdFile(const std::string &path, const std::string &nonce, const void *
     const std::string tmp = path + ".tmp" + std::to_string((long long)getpid());
     FILE *f = std::fopen(tmp.c_str(), "wb");
     if (!f) return false;
-    const uint32_t n = (uint32_t)nonce.size();
-    bool ok = std::fwrite(kIdMagic, sizeof(kIdMagic), 1, f) == 1 && std::fwrite(&n, sizeof(n), 1, f) == 1 &&
-              (n == 0 || std::fwrite(nonce.data(), n, 1, f) == 1) && std::fwrite(id, size, 1, f) == 1;
+    const int64_t pid = (int64_t)getpid();
+    const uint64_t start = proc_start_ticks((long)pid);
+    bool ok = std::fwrite(kIdMagic, sizeof(kIdMagic), 1, f) == 1 && write_str(f, nonce) && write_str(f, host_name()) &&
+              std::fwrite(&pid, sizeof(pid), 1, f) == 1 && std::fwrite(&start, sizeof(start), 1, f) == 1 &&
+              std::fwrite(id, size, 1, f) == 1;
     ok = std::fclose(f) == 0 && ok;
     if (!ok) {
         (void)std::remove(tmp.c_str());
@@ -118,13 +145,21 @@ int ReadIdFile(const std::string &path, const std::string &nonce, void *id, size
     FILE *f = std::fopen(path.c_str(), "rb");
     if (!f) return 0;
     char magic[8];
-    uint32_t n = 0;
+    std::string got, host;
+    int64_t pid = 0;
+    uint64_t start = 0;
     int r = -1;
     if (std::fread(magic, sizeof(magic), 1, f) == 1 && std::memcmp(magic, kIdMagic, sizeof(magic)) == 0 &&
-        std::fread(&n, sizeof(n), 1, f) == 1 && n == nonce.size()) {
-        std::string got(n, '\0');
-        if ((n == 0 || std::fread(got.data(), n, 1, f) == 1) && got == nonce)
-            r = std::fread(id, size, 1, f) == 1 ? 1 : 0;
+        read_str(f, got, 4096) && got == nonce) {
+        // the rest may still be missing (a torn file reads as absent, the reader waits)
+        if (read_str(f, host, 255) && std::fread(&pid, sizeof(pid), 1, f) == 1 &&
+            std::fread(&start, sizeof(start), 1, f) == 1 && std::fread(id, size, 1, f) == 1) {
+            // a writer on this host must still run (rank 0 waits in ncclCommInitRank until every
+            // rank has joined); on a shared filesystem another host's writer is taken on its nonce
+            r = host != host_name() || (start != 0 && proc_start_ticks((long)pid) == start) ? 1 : -1;
+        } else {
+            r = 0;
+        }
     }
     std::fclose(f);
     return r;
@@ -141,6 +176,7 @@ DistInfo DistFromEnv() noexcept {
 
 FrameGather::~FrameGather() noexcept {
     Release();
+    if (m_host && m_info.rank == 0) (void)rmdir(m_dir.c_str());  // empty once every frame was consumed
     if (m_comm) (void)ncclCommDestroy(m_comm);
 }
 
@@ -149,13 +185,27 @@ void FrameGather::Release() noexcept {
         if (p) (void)hipFree(p);
     for (auto *p : m_staging)
         if (p) (void)hipFree(p);
+    for (auto *p : m_pinned)
+        if (p) (void)hipHostFree(p);
     m_maps.clear();
     m_staging.clear();
+    m_pinned.clear();
 }
 
 bool FrameGather::Init(const DistInfo &d, int device, const std::string &id_path) noexcept {
     m_info = d;
     if (hipSetDevice(device) != hipSuccess) return false;
+    if (const char *tr = std::getenv("PUPIL_GATHER_TRANSPORT"); tr && std::strcmp(tr, "host") == 0) {
+        // test transport (dist.h): a per-launch directory instead of a communicator
+        m_host = true;
+        m_dir = id_path + ".d";
+        if (mkdir(m_dir.c_str(), 0700) != 0 && errno != EEXIST) {
+            Log("rank %d: cannot create %s", d.rank, m_dir.c_str());
+            return false;
+        }
+        Log("rank %d of %d: host-staged tile gather through %s (test transport)", d.rank, d.world, m_dir.c_str());
+        return true;
+    }
     ncclUniqueId id;
     if (!exchange_id(d, id_path, id)) {
         Log("rank %d: RCCL unique id exchange through %s failed", d.rank, id_path.c_str());
@@ -182,24 +232,84 @@ bool FrameGather::Setup(uint32_t width, uint32_t height) noexcept {
         if (pupil_pt_local_pixels(width, height, m_info.tile, r, world, nullptr, &n) != PUPIL_OK) return false;
         m_counts[r] = n;
     }
-    if (m_info.rank != 0) return true;
+    if (m_info.rank != 0) {
+        if (!m_host) return true;
+        m_pinned.assign(1, nullptr);  // this rank's tiles on their way to the exchange file
+        return hipHostMalloc((void **)&m_pinned[0], sizeof(float4) * std::max(1u, m_counts[(size_t)m_info.rank])) ==
+               hipSuccess;
+    }
     m_maps.assign(world, nullptr);
     m_staging.assign(world, nullptr);
+    if (m_host) m_pinned.assign(world, nullptr);
     for (uint32_t r = 0; r < world; r++) {
         std::vector<uint32_t> map(std::max(1u, m_counts[r]));
         uint32_t n = m_counts[r];
         if (pupil_pt_local_pixels(width, height, m_info.tile, r, world, map.data(), &n) != PUPIL_OK) return false;
         if (hipMalloc((void **)&m_maps[r], sizeof(uint32_t) * map.size()) != hipSuccess ||
             hipMemcpy(m_maps[r], map.data(), sizeof(uint32_t) * map.size(), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMalloc((void **)&m_staging[r], sizeof(float4) * map.size()) != hipSuccess)
+            hipMalloc((void **)&m_staging[r], sizeof(float4) * map.size()) != hipSuccess ||
+            (m_host && r > 0 && hipHostMalloc((void **)&m_pinned[r], sizeof(float4) * map.size()) != hipSuccess))
             return false;
     }
     return true;
 }
 
-bool FrameGather::Gather(const void *local, void *full, hipStream_t stream) noexcept {
-    if (!m_comm) return false;
+// Test transport: rank r != 0 copies its tiles to pinned memory and publishes them as
+// <dir>/f<r>_<frame> (complete temporary renamed into place), after rank 0 consumed its
+// previous frame; rank 0 waits for every rank's file of this frame, uploads it into the
+// staging buffer and removes it.  Every wait is bounded (120 s).
+bool FrameGather::GatherHost(const void *local, hipStream_t stream) noexcept {
     const int world = m_info.world;
+    auto name = [&](int r, uint64_t f) { return m_dir + "/f" + std::to_string(r) + "_" + std::to_string(f); };
+    auto wait_for = [&](const std::string &path, bool present) {
+        const auto t0 = std::chrono::steady_clock::now();
+        struct stat st;
+        while ((stat(path.c_str(), &st) == 0) != present) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) return false;
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+        return true;
+    };
+    const uint64_t frame = m_frame++;
+    if (m_info.rank != 0) {
+        const size_t bytes = sizeof(float4) * m_counts[(size_t)m_info.rank];
+        if (frame > 0 && !wait_for(name(m_info.rank, frame - 1), false)) return false;
+        if (hipMemcpyAsync(m_pinned[0], local, bytes, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+            hipStreamSynchronize(stream) != hipSuccess)
+            return false;
+        const std::string tmp = name(m_info.rank, frame) + ".tmp";
+        FILE *f = std::fopen(tmp.c_str(), "wb");
+        if (!f) return false;
+        const bool written = bytes == 0 || std::fwrite(m_pinned[0], bytes, 1, f) == 1;
+        const bool closed = std::fclose(f) == 0;
+        return written && closed && std::rename(tmp.c_str(), name(m_info.rank, frame).c_str()) == 0;
+    }
+    for (int r = 1; r < world; r++) {
+        const size_t bytes = sizeof(float4) * m_counts[(size_t)r];
+        const std::string path = name(r, frame);
+        if (!wait_for(path, true)) {
+            Log("rank 0: no tiles from rank %d for frame %llu", r, (unsigned long long)frame);
+            return false;
+        }
+        FILE *f = std::fopen(path.c_str(), "rb");
+        const bool ok = f && (bytes == 0 || std::fread(m_pinned[(size_t)r], bytes, 1, f) == 1);
+        if (f) std::fclose(f);
+        (void)std::remove(path.c_str());
+        if (!ok || hipMemcpyAsync(m_staging[(size_t)r], m_pinned[(size_t)r], bytes, hipMemcpyHostToDevice, stream) !=
+                       hipSuccess)
+            return false;
+    }
+    // the pinned buffers are rewritten by the next frame's reads: the uploads must have run
+    return hipStreamSynchronize(stream) == hipSuccess;
+}
+
+bool FrameGather::Gather(const void *local, void *full, hipStream_t stream) noexcept {
+    const int world = m_info.world;
+    if (m_host) {
+        if (!GatherHost(local, stream)) return false;
+        return m_info.rank != 0 || Scatter(local, full, stream);
+    }
+    if (!m_comm) return false;
     if (ncclGroupStart() != ncclSuccess) return false;
     bool posted = true;
     if (m_info.rank == 0) {
@@ -212,8 +322,13 @@ bool FrameGather::Gather(const void *local, void *full, hipStream_t stream) noex
     }
     // the group is closed on every path (an open group would swallow the next RCCL calls)
     if (ncclGroupEnd() != ncclSuccess || !posted) return false;
-    if (m_info.rank != 0) return true;
-    for (int r = 0; r < world; r++) {
+    return m_info.rank != 0 || Scatter(local, full, stream);
+}
+
+// rank 0: every rank's compact tiles (its own from `local`, the others' received into the
+// staging buffers) into the full frame, one kernel per rank
+bool FrameGather::Scatter(const void *local, void *full, hipStream_t stream) noexcept {
+    for (int r = 0; r < m_info.world; r++) {
         const uint32_t n = m_counts[(size_t)r];
         if (!n) continue;
         const float4 *src = r == 0 ? static_cast<const float4 *>(local) : reinterpret_cast<const float4 *>(m_staging[(size_t)r]);

@@ -138,6 +138,43 @@ def test_example_rccl_tile_gather_single_rank_matches():
     assert np.array_equal(_read_pfm(plain), _read_pfm(dist))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_example_ranks_on_one_gpu_match_one_rank(world):
+    """The C++ drop-in's rank != 0 code (PTPass::SetScene's compact tile buffers,
+    FrameGather's send side) with `world` rank processes sharing this box's one GPU over the
+    host-staged test transport (PUPIL_GATHER_TRANSPORT=host; RCCL refuses two ranks on one
+    device): every rank renders its tiles of every OnRun, rank 0 gathers and scatters them, and
+    its saved image equals the single-rank run bit for bit."""
+    _built()
+    from pupiloptixlab_amd import scenes
+
+    os.makedirs(TMP, exist_ok=True)
+    xml = scenes.cornell_xml(os.path.join(TMP, "cb_ranks.xml"), 80, 56, 4)  # ragged 32-px tiles
+    plain, multi = os.path.join(TMP, "cb_ranks_1.pfm"), os.path.join(TMP, f"cb_ranks_{world}.pfm")
+    r = subprocess.run([EXE, xml, "5", plain], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    port = str(_free_port())
+    procs = []
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, PUPIL_GATHER_TRANSPORT="host", PUPIL_RCCL_NONCE=f"ranks-test-{port}")
+        procs.append(subprocess.Popen([EXE, xml, "5", multi], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True, env=env))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=240))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e
+    assert all("host-staged tile gather" in e for _, e in outs)
+    assert np.array_equal(_read_pfm(plain).view(np.uint32), _read_pfm(multi).view(np.uint32))
+
+
 def test_framework_links_rccl():
     _built()
     out = subprocess.run(["ldd", FW], capture_output=True, text=True, check=True).stdout
@@ -181,6 +218,29 @@ def test_rccl_id_file_rejects_a_stale_launch(tmp_path, monkeypatch):
     monkeypatch.setenv("TORCHELASTIC_RUN_ID", "b")
     assert lib.pupil_dist_id_path(out, 512) == 0
     assert pa.startswith(b"/tmp/pupil_rccl_29511_") and out.value != pa
+
+
+def test_rccl_id_file_of_a_finished_writer_is_stale(tmp_path):
+    """A file with this launch's nonce whose writer (on this host) no longer runs -- a crashed
+    or finished earlier launch with the same launch environment -- is never used, however
+    recently it was written; the live writer's file is accepted however long ago it was
+    written (no wall clocks compared: ranks may start any time apart)."""
+    _built()
+    import ctypes as C
+    import sys
+
+    path = str(tmp_path / "pupil_rccl.id")
+    code = ("import ctypes as C; lib = C.CDLL(%r); lib.pupil_dist_write_id_file.argtypes = [C.c_char_p, C.c_char_p, "
+            "C.c_void_p]; assert lib.pupil_dist_write_id_file(%r, b'launch-x', bytes(128)) == 0" % (FW, path.encode()))
+    subprocess.run([sys.executable, "-c", code], check=True)  # the writer exits
+    lib = C.CDLL(FW)
+    lib.pupil_dist_write_id_file.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p]
+    lib.pupil_dist_read_id_file.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p]
+    buf = C.create_string_buffer(128)
+    assert lib.pupil_dist_read_id_file(path.encode(), b"launch-x", buf) == -1
+    assert lib.pupil_dist_write_id_file(path.encode(), b"launch-x", bytes(range(128))) == 0  # this process: alive
+    os.utime(path, (1, 1))  # an mtime decades old changes nothing
+    assert lib.pupil_dist_read_id_file(path.encode(), b"launch-x", buf) == 1 and buf.raw == bytes(range(128))
 
 
 def test_rccl_id_path_agrees_across_differently_started_ranks():

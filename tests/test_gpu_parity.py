@@ -766,6 +766,18 @@ def test_moving_camera_cadence_starts_no_frames_ahead():
         ref = oracle.OracleScene(d).render(spp=1)["accum"]
         got = pt.buffers.get("pt accum buffer").cpu().numpy()
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+    # ... and that footprint (path state, queues, AOV scratch) is exactly the one of an engine
+    # that never pipelines (PUPIL_AHEAD=0, read at create)
+    os.environ["PUPIL_AHEAD"] = "0"
+    try:
+        pt0 = PTPass(device=0)
+        pt0.set_scene(desc)
+        pt0.render(1)
+        torch.cuda.synchronize()
+        assert pt0.stats()["ring_bytes"] == ring0
+        pt0.close_engine()
+    finally:
+        del os.environ["PUPIL_AHEAD"]
     for _ in range(3):  # the camera stops: the OnRuns continue each other and pipeline
         pt.render(1)
     torch.cuda.synchronize()

@@ -63,10 +63,13 @@ def traffic_json(root, kernels, out_path, note=""):
     # rays the plain traversal kernels traced in each pass (bench.py's JSON line,
     # config.rays_traced_plain_process): identical work in every pass
     rays = set()
+    simd = None  # the bench line's SIMD efficiency of the traversal (counter frame, same in every pass)
     for lg in sorted(glob.glob(os.path.join(root, "p*.log"))):
         for line in open(lg):
             if line.startswith("{") and '"metric"' in line:
-                rays.add(json.loads(line)["config"].get("rays_traced_plain_process"))
+                bl = json.loads(line)
+                rays.add(bl["config"].get("rays_traced_plain_process"))
+                simd = (bl.get("roofline") or {}).get("simd_efficiency") or simd
     rays.discard(None)
     assert len(rays) <= 1, f"passes traced different ray counts: {rays}"
     n_rays = rays.pop() if rays else None
@@ -91,6 +94,7 @@ def traffic_json(root, kernels, out_path, note=""):
            "traffic_bytes_per_ray": (2.0 * total("FETCH_SIZE") + total("WRITE_SIZE")) * 1024.0 / n_rays if n_rays else None,
            "valu_insts_per_ray": total("SQ_INSTS_VALU") / n_rays if n_rays and valu else None,
            "dispatches": len(d),
+           "simd_efficiency": simd,
            "note": note}
     with open(out_path, "w") as fh:
         json.dump(rec, fh, indent=1)
