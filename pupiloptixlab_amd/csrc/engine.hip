@@ -1378,15 +1378,17 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
         if (pt->last_stats) {
             unsigned long long tc[32];
             HIP_TRY(hipMemcpy(tc, pt->trace_counters, sizeof(tc), hipMemcpyDeviceToHost));
-            for (int k = 0; k < 2 && std::getenv("PUPIL_TRACE_DIAG"); k++) {  // SIMD efficiency, persistent kernels
-                const unsigned long long *d = tc + 2 + 6 * k;
-                if (!d[0]) continue;
+            if (std::getenv("PUPIL_TRACE_DIAG") && tc[2]) {  // SIMD efficiency, persistent kernels
+                const unsigned long long *d = tc + 2;
+                const double visits = (double)std::max(1ull, tc[0] + tc[14]);
                 std::fprintf(stderr,
-                             "[pupil] %s: node loop %llu wave-iters, %.1f%% lanes active; leaf loop %llu wave-iters, "
-                             "%.1f%% lanes active; %llu refills, %.1f lanes each\n",
-                             k ? "shadow" : "extend", d[0], 100.0 * (double)d[1] / (64.0 * (double)d[0]), d[2],
+                             "[pupil] traversal: node loop %llu wave-iters, %.1f%% lanes active; leaf loop %llu wave-iters, "
+                             "%.1f%% lanes active; %llu refills, %.1f lanes each; node visits %.0f, %.1f%% with no child "
+                             "hit, %.1f%% of a popped node already beyond tmax\n",
+                             d[0], 100.0 * (double)d[1] / (64.0 * (double)d[0]), d[2],
                              100.0 * (double)d[3] / (64.0 * (double)std::max(1ull, d[2])), d[4],
-                             (double)d[5] / (double)std::max(1ull, d[4]));
+                             (double)d[5] / (double)std::max(1ull, d[4]), visits, 100.0 * (double)tc[9] / visits,
+                             100.0 * (double)tc[8] / visits);
             }
             c.node_loop_iters = tc[2];  // trace4_body dg[0..5]
             c.node_loop_lanes = tc[3];

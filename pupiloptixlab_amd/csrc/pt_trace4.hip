@@ -46,19 +46,24 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
 template <int MODE, bool ANY, bool STATS, bool TL>
 __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathState &ps, const Queues &q,
                                             const TraceJob &job, int *ovf, uint32_t ovf_threads,
-                                            const TraceStats &stats, int *s_ring, float *s_aux) {
+                                            const TraceStats &stats, int *s_ring, float *s_aux, float *s_tst) {
     constexpr float kInf = __builtin_huge_valf();
     constexpr bool kMixed = MODE == kModeMixed || MODE == kModeMixedAhead;
     const uint32_t n_next = kMixed ? q.counts[kCntNext] : 0u;
     // mixed launches may carry the next render's camera rays (render-ahead, TraceJob::ahead_off)
     const uint32_t n_ahead = MODE == kModeMixedAhead ? job.static_count : 0u;
     const uint32_t count = kMixed ? n_next + q.counts[kCntShadow] : (job.count_ptr ? *job.count_ptr : job.static_count);
-    RingStack st;
+    LinStack st;
     st.lds = s_ring + threadIdx.x;
     st.ovf_blk = ovf + blockIdx.x * blockDim.x;
     st.lds0 = s_ring;
     st.ovf_stride = ovf_threads;
+    if (STATS) st.tcol = s_tst + threadIdx.x;
     st.reset();
+    // STATS: visits of a popped node whose entry distance already exceeds the ray's tmax (a
+    // stack holding distances could skip them without the fetch), visits where no child was hit
+    uint32_t n_cullable = 0, n_nohit = 0;
+    float t_node = 0.f;
     uint32_t nv = 0, npt = 0, nv_sh = 0, npt_sh = 0;  // mixed: shadow-ray counts apart
     uint32_t n_unique = 0;  // STATS: distinct node fetches (per wave step)
     // STATS-only SIMD-efficiency diagnostics, each event counted by one lane:
@@ -238,18 +243,25 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 int l[4];
                 if (TL) visit4(n, bo, bi, be, tmin, tmax, t, l);
                 else visit4(n, r.o, r.idir, be, tmin, tmax, t, l);
+                if (STATS) {
+                    n_cullable += t_node > tmax ? 1u : 0u;
+                    n_nohit += t[0] == kInf ? 1u : 0u;
+                }
                 if (t[0] == kInf) {
                     node = st.pop();
+                    if (STATS) t_node = st.tpop;
                 } else {
                     node = l[0];
+                    if (STATS) t_node = t[0];
                     st.reserve3();
-                    st.push(l[3], t[3] != kInf);
-                    st.push(l[2], t[2] != kInf);
-                    st.push(l[1], t[1] != kInf);
+                    st.push3t(t[1], t[2], t[3], t[2] != kInf, t[3] != kInf);
+                    st.push3(l[1], l[2], l[3], t[1] != kInf, t[2] != kInf, t[3] != kInf);
+                    if (node == kEmptyLink) node = st.pop();  // degenerate child boxes only (LinStack)
                 }
                 if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
                     leaf = node;
                     node = st.pop();
+                    if (STATS) t_node = st.tpop;
                 }
                 // leave for the leaf phase once fewer than node_min lanes still need a node
                 if ((uint32_t)__popcll(__ballot(leaf >= 0)) < job.node_min) break;
@@ -283,8 +295,8 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         }
                     } else {  // enter its BLAS; the pending TLAS link resumes after kReturnLink
                         st.reserve3();
-                        st.push(node, true);
-                        st.push(kReturnLink, true);
+                        st.push(node);
+                        st.push(kReturnLink);
                         in_blas = true;
                         inst = id;
                         enter_instance(in, r, ray_dir(), tmax, sc.node_bound, bo, bi, be);
@@ -297,11 +309,11 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         continue;
                     }
                 } else if (TL) {
-                    if (intersect_leaf_tl<STATS>(sc, r, leaf, inst, tmin, tmax, best_key, best_idx, b1, b2, np_cnt,
-                                                 found, any))
+                    if (intersect_leaf_tl<STATS>(sc, r, leaf, inst, tmin, tmax, best_key, best_idx, b1, b2,
+                                                 np_cnt, found, any))
                         break;
-                } else if (intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, np_cnt,
-                                                     found, any, ray_dir)) {
+                } else if (intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2,
+                                                     np_cnt, found, any, ray_dir)) {
                     break;
                 }
                 leaf = node;
@@ -363,6 +375,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     flush_stats<STATS>(&stats, nv, npt, 0);
     if (kMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
     flush_stats<STATS>(&stats, n_unique, 0u, 18);
+    flush_stats<STATS>(&stats, n_cullable, n_nohit, 8);
     if (STATS && stats.wave_times && lane_id() == 0) {
         unsigned long long *w = stats.wave_times + 4ull * (blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u);
         w[0] = t_start;
@@ -406,7 +419,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
     __shared__ int s_ring[kRing * kTraceBlock];
     __shared__ float s_aux[4 * kTraceBlock];
-    trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux);
+    __shared__ float s_tst[STATS ? kRing * kTraceBlock : 1];
+    trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst);
 }
 
 // two-level variant: 9 more live registers (object-space box ray, margin,
@@ -416,7 +430,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
     __shared__ int s_ring[kRing * kTraceBlock];
     __shared__ float s_aux[4 * kTraceBlock];
-    trace4_body<MODE, ANY, STATS, true>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux);
+    __shared__ float s_tst[STATS ? kRing * kTraceBlock : 1];
+    trace4_body<MODE, ANY, STATS, true>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst);
 }
 
 

@@ -128,53 +128,91 @@ __device__ __forceinline__ void flush_stats(const TraceStats *stats, uint32_t nv
 // and pull rays from the queue with one atomic per wave; a lane whose ray has
 // terminated is refilled as soon as `refill` lanes of its wave are idle
 // (Aila & Laine 2009, "dynamic fetch"), so a wave never idles on its longest
-// ray.  The stack is a 16-entry LDS ring per lane that spills its oldest 8
+// ray.  The stack is a 16-entry LDS column per lane that spills its bottom 8
 // entries to HBM when full, so push/pop are LDS-only in the common case.
 constexpr int kSpill = 8;
-static_assert((kRing & (kRing - 1)) == 0, "ring size must be a power of two");
 
-struct RingStack {
+// Entries [0, sp) of the LDS column in order, [0, nsp) in the overflow column (r05: replaces
+// r01-r04's ring with a wrap mask and three conditional pushes, 141 -> 132 VALU per node visit
+// with a hit, launch time unchanged: profiles/r05_stack_ab.txt).  A visit's pushes are three unconditional
+// stores at sp, sp + 1, sp + 2 of the hit children's links in push order (far to near; the
+// slots above the new top are harmless) and one add, instead of three conditional pushes;
+// a full column spills its bottom 8 entries and moves the top ones down (rare: deep trees).
+// Popping an empty child slot (kEmptyLink, possible only for degenerate child boxes whose
+// empty planes the conservative slab bound lets through) pops again.
+struct LinStack {
     int *lds;  // this lane's column (stride kTraceBlock)
-    // the overflow column is found from the block's base and the lane's LDS column only
-    // when the ring spills or refills (no 64-bit per-lane pointer held across the loop)
-    int *ovf_blk;       // this block's first overflow column (uniform)
-    const int *lds0;    // the block's ring base (uniform)
+    int *ovf_blk;
+    const int *lds0;
     __device__ __forceinline__ int *ovf_col() {
         uint32_t lane;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"((uint32_t)(lds - lds0)));  // not hoisted out of the loop
+        asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"((uint32_t)(lds - lds0)));
         return ovf_blk + lane;
     }
     uint32_t ovf_stride;
-    int sp;   // logical entries [0, sp)
-    int bot;  // entries [0, bot) live in ovf, [bot, sp) in the ring
+    int sp;   // entries in the LDS column
+    int nsp;  // entries in the overflow column (multiple of kSpill)
+    // counter kernels only (null otherwise, compiled out): the entry distance of every LDS
+    // entry in a parallel column, so a pop can tell whether the node lies beyond the ray's
+    // current tmax (PUPIL_TRACE_DIAG "cullable visits"); entries reloaded from the overflow
+    // column read 0 (unknown)
+    float *tcol = nullptr;
+    float tpop = 0.f;  // the last popped entry's distance
 
-    __device__ __forceinline__ int &slot(int i) { return lds[(i & (kRing - 1)) * kTraceBlock]; }
-    __device__ __forceinline__ void reset() { sp = bot = 0; }
-    // Make room for three pushes.  The overflow column holds kStackOvf entries;
-    // create() rejects trees needing more than kTraceStackEntries (3 per BVH4
-    // level + 2 per instance entry), so the guard below never triggers.
+    __device__ __forceinline__ int &slot(int i) { return lds[i * kTraceBlock]; }
+    __device__ __forceinline__ void reset() { sp = nsp = 0; }
     __device__ __forceinline__ void reserve3() {
-        if (sp + 3 - bot > kRing && bot + kSpill <= kStackOvf) {
+        if (sp > kRing - 3 && nsp + kSpill <= kStackOvf) {
             int *ovf = ovf_col();
 #pragma unroll
-            for (int k = 0; k < kSpill; k++) ovf[(uint32_t)(bot + k) * ovf_stride] = slot(bot + k);
-            bot += kSpill;
+            for (int k = 0; k < kSpill; k++) ovf[(uint32_t)(nsp + k) * ovf_stride] = slot(k);
+#pragma unroll
+            for (int k = kSpill; k < kRing; k++)
+                if (k < sp) {
+                    slot(k - kSpill) = slot(k);
+                    if (tcol) tcol[(k - kSpill) * kTraceBlock] = tcol[k * kTraceBlock];
+                }
+            nsp += kSpill;
+            sp -= kSpill;
         }
     }
-    __device__ __forceinline__ void push(int v, bool keep) {
-        slot(sp) = v;  // harmless above the top when !keep
-        sp += keep ? 1 : 0;
+    __device__ __forceinline__ void push(int v) {
+        if (tcol) tcol[sp * kTraceBlock] = 0.f;
+        slot(sp++) = v;
     }
-    __device__ __forceinline__ int pop() {
-        if (sp == 0) return kSentinel;
-        sp--;
-        if (sp < bot) {
-            bot -= kSpill;
+    __device__ __forceinline__ void push3t(float t1, float t2, float t3, bool c2, bool c3) {
+        if (!tcol) return;
+        tcol[sp * kTraceBlock] = c3 ? t3 : (c2 ? t2 : t1);
+        tcol[(sp + 1) * kTraceBlock] = c3 ? t2 : t1;
+        tcol[(sp + 2) * kTraceBlock] = t1;
+    }
+    // the hit children of positions 1..3 of a sorted visit (c1 >= c2 >= c3: hits first)
+    __device__ __forceinline__ void push3(int l1, int l2, int l3, bool c1, bool c2, bool c3) {
+        slot(sp) = c3 ? l3 : (c2 ? l2 : l1);
+        slot(sp + 1) = c3 ? l2 : l1;
+        slot(sp + 2) = l1;
+        sp += (c1 ? 1 : 0) + (c2 ? 1 : 0) + (c3 ? 1 : 0);
+    }
+    __device__ __forceinline__ int pop_raw() {
+        if (sp == 0) {
+            if (nsp == 0) return kSentinel;
+            nsp -= kSpill;
             const int *ovf = ovf_col();
 #pragma unroll
-            for (int k = 0; k < kSpill; k++) slot(bot + k) = ovf[(uint32_t)(bot + k) * ovf_stride];
+            for (int k = 0; k < kSpill; k++) {
+                slot(k) = ovf[(uint32_t)(nsp + k) * ovf_stride];
+                if (tcol) tcol[k * kTraceBlock] = 0.f;
+            }
+            sp = kSpill;
         }
+        --sp;
+        if (tcol) tpop = tcol[sp * kTraceBlock];
         return slot(sp);
+    }
+    __device__ __forceinline__ int pop() {
+        int v = pop_raw();
+        while (v == kEmptyLink) v = pop_raw();
+        return v;
     }
 };
 
@@ -275,7 +313,7 @@ __device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, v
                                      __builtin_fmaf(ubyte(fz, k), bz, farz)),
                                tmax);
         l[k] = n.child[k];
-        t[k] = (tn <= tf && l[k] != kEmptyLink) ? tn : kInf;
+        t[k] = tn <= tf ? tn : kInf;  // an empty slot (planes 255 / 0) passes only for degenerate boxes: LinStack
     }
     csel(t[0], l[0], t[1], l[1]);
     csel(t[2], l[2], t[3], l[3]);
