@@ -302,6 +302,9 @@ typedef struct pupil_pt_counters {
     uint64_t leaf_loop_lanes;
     uint64_t refills;
     uint64_t refill_lanes;
+    /* renders run as one persistent launch per frame (renders that start no frame ahead and
+     * have at most PUPIL_FRAME_PATHS paths: the moving-camera OnRun, one rank's tiles) */
+    uint64_t frame_launches;
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;

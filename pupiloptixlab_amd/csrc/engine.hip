@@ -125,8 +125,14 @@ struct pupil_pt {
     size_t pipe_cap = 0;              // paths per ring slot (G frames)
     // PUPIL_PIPE_GROUP_PATHS: renders of fewer paths batch G = ceil(this / paths) frames per slot
     double pipe_group_paths = 8e6;
+    // renders that start no frame ahead (a moving camera) with at most this many paths run as one
+    // persistent launch per frame (pt_frame.hip); PUPIL_FRAME_PATHS, 0 = never.  Moving-camera
+    // OnRuns at 1080p (r05 shard probe): one rank of 8 (260 k paths) 7.40 vs 8.47 ms per 8 OnRuns
+    // in one launch vs the stage pipeline, one of 4 (518 k) 12.86 vs 10.56, one GPU 39.7 vs 22.8
+    double frame_paths = 4e5;
     bool ring_fresh = true;           // the ring was (re)allocated: its flags bytes are not yet cleared
     uint32_t pipe_run = 0;            // consecutive renders that continued the previous one
+    uint64_t frame_launches = 0;      // renders run as one persistent launch (pt_frame.hip)
     uint32_t pipe_next_seed = 0;      // random_seed of the render that would continue the last one
     uint32_t pipe_gen = 0;            // iterations so far (flags tags)
     uint32_t pipe_limit = 0;          // PUPIL_PIPE: most slots (0 = max_depth)
@@ -672,6 +678,28 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         return (uint32_t)e;
     };
     const uint32_t interleave0 = pt->primary_interleave;
+    // a render that starts nothing ahead and needs no frame in flight, small enough (one rank's
+    // tiles, small films): the whole frame in one persistent launch (pt_frame.hip), no
+    // per-bounce traversal drain, shade launch or partition
+    if (pt->frame_paths > 0.0 && !cx.stats && !speculate && pt->pipe.empty() && (double)np <= pt->frame_paths &&
+        frame_kernel_supported(pt->sc)) {
+        // this render's extension / shadow rays = the growth of the running totals from here
+        HIP_TRY(hipMemcpyAsync(pt->ray_cum + 2, pt->ray_cum, 2 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
+        pt->snap_taken = true;
+        FrameParams fs = fp;
+        fs.group = 1;
+        cx.ev0(1);
+        launch_frame(pt->sc, fs, ring, pt->q.work + kWorkFrame, pt->ray_cum, pt->ovf, pt->ovf_threads,
+                     interleave0 && fp.spp > 1 ? fp.spp : 0u, s);
+        cx.ev1();
+        launch_accumulate(fp, ring, nullptr, true, s);
+        pt->pipe_next_seed = launch->random_seed + fp.spp;
+        pt->last_iters = D;
+        pt->last_primary = np;
+        pt->primary_cum += np;
+        pt->frame_launches++;
+        return PUPIL_OK;
+    }
     // iterations this render needs: none when an earlier render completed its frame
     const uint32_t L = pt->pipe.empty() ? D : D - pt->pipe.front().phases;
     // AOV scratch of ring slot `slot`, frame `f` of its group: 7 floats per local pixel
@@ -1013,6 +1041,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
     if (const char *g = std::getenv("PUPIL_PIPE_PATHS")) pt->pipe_paths = std::max(1.0, std::atof(g));
     if (const char *g = std::getenv("PUPIL_PIPE_GROUP_PATHS")) pt->pipe_group_paths = std::max(1.0, std::atof(g));
+    if (const char *g = std::getenv("PUPIL_FRAME_PATHS")) pt->frame_paths = std::max(0.0, std::atof(g));
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));
     if (nodes4_count(pt) > kMaxNodes4)
@@ -1322,6 +1351,7 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
     c.ring_bytes = pt->ring_bytes + sizeof(float) * (uint64_t)pt->aov_cap;
     c.ring_budget_bytes = (uint64_t)pt->pipe_budget;
     c.accel_refits = pt->refits;
+    c.frame_launches = pt->frame_launches;
     for (int a = 0; a < 3; a++) c.node_bound[a] = pt->sc.node_bound[a];
     if (pt->last_paths) {
         // rays traced by the last render's launches (pipelined renders: of every frame in

@@ -61,8 +61,8 @@ constexpr uint32_t kCntNext = 9, kCntShadow = 10;                      // queue 
 // own 128-B line.  Zero at allocation; the last wave of every persistent launch
 // puts them back to zero.
 constexpr uint32_t kWorkShards = 8, kWorkStride = 32, kWorkKind = (2 * kWorkShards + 1) * kWorkStride;
-constexpr uint32_t kWorkExtend = 0, kWorkShadow = kWorkKind, kWorkRays = 2 * kWorkKind;
-constexpr uint32_t kWorkSlots = 3 * kWorkKind;
+constexpr uint32_t kWorkExtend = 0, kWorkShadow = kWorkKind, kWorkRays = 2 * kWorkKind, kWorkFrame = 3 * kWorkKind;
+constexpr uint32_t kWorkSlots = 4 * kWorkKind;
 constexpr uint32_t kStartBins = 16;                                    // [16..24] material bin starts
 constexpr uint32_t kStartNext = 25, kStartShadow = 26;                 // next / shadow regions of nxsh
 constexpr uint32_t kScratch = 27;
@@ -174,6 +174,12 @@ void launch_shade(const DeviceScene &sc, const FrameParams &fp, const PathState 
 void launch_trace_mixed(const DeviceScene &sc, const PathState &ps, const Queues &q, int *ovf, uint32_t ovf_threads,
                         const TraceStats *stats, hipStream_t s, uint32_t ahead_count = 0, uint32_t list_base = 0,
                         uint32_t ahead_base = 0, uint32_t ahead_spp = 0, uint32_t ahead_local = 0);
+// small frames (pt_frame.hip): every path of the frame -- camera ray, bounces, shadow rays --
+// in one persistent launch (no partitions, one drain); the accumulate follows.  Flat BVH4 and
+// two-level world mode only.  ray_cum: running totals of extension [0] and shadow [1] rays.
+bool frame_kernel_supported(const DeviceScene &sc);
+void launch_frame(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, uint32_t *work,
+                  unsigned long long *ray_cum, int *ovf, uint32_t ovf_threads, uint32_t interleave_spp, hipStream_t s);
 // running mean of the batch's frames into fp.accum / fp.frame; aov_src (or null): the
 // frame's AOVs from the slot scratch (3n albedo, 3n normal, n test floats) copied to the
 // outputs; clear_flags: zero the frame's flags bytes (its ring slot is free again)

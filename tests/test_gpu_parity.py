@@ -25,7 +25,7 @@ def rel_l2(a, b):
     return float(np.sqrt(((a - b) ** 2).sum() / max(1e-30, (b ** 2).sum())))
 
 
-def render_gpu(desc, spp, seed=0, cnt=0, max_depth=0, accumulate=True, tile=(32, 0, 1), prev=None):
+def render_gpu(desc, spp, seed=0, cnt=0, max_depth=0, accumulate=True, tile=(32, 0, 1), prev=None, stats=True):
     import torch
     from pupiloptixlab_amd.pt_pass import PTPass
 
@@ -40,7 +40,7 @@ def render_gpu(desc, spp, seed=0, cnt=0, max_depth=0, accumulate=True, tile=(32,
     pt.random_seed, pt.sample_cnt = seed, cnt
     if prev is not None:
         pt.buffers.get("pt accum buffer").copy_(torch.from_numpy(prev))
-    pt.render(spp, collect_stats=True)
+    pt.render(spp, collect_stats=stats)
     torch.cuda.synchronize()
     out = {k: pt.buffers.get(k).cpu().numpy() for k in ("pt accum buffer", "final result", "albedo", "normal", "test")}
     out["stats"] = pt.stats()
@@ -177,6 +177,7 @@ def test_stage_schedules_parity(node_min, monkeypatch):
     """The mixed extension + shadow launch with the node phase left at 1, 8 (default) or 64
     active lanes: lanes switch between node and leaf phases at other points, hits do not change."""
     monkeypatch.setenv("PUPIL_NODE_MIN", node_min)
+    monkeypatch.setenv("PUPIL_FRAME_PATHS", "0")  # the stage launches, not the one-launch frame
     desc = scenes.sphere_field(27, 200, 120, 5, seed=4).desc()
     gpu = render_gpu(desc, 3)
     ref = oracle.OracleScene(desc).render(spp=3)
@@ -362,6 +363,50 @@ def test_tile_sharding_matches_full_frame():
         seen[pix] = True
     assert seen.all()
     assert np.array_equal(got, full)
+
+
+@pytest.mark.parametrize("case", ["cornell", "cornell_spp3_depth7", "materials", "materials_two_level", "field",
+                                  "field_tiles", "field_stages"])
+def test_one_launch_frames_match_oracle(case, monkeypatch):
+    """Renders that start no frame ahead and are small (PUPIL_FRAME_PATHS) run as ONE persistent
+    launch per frame (pt_frame.hip): per-wave rounds of traversal (a bounce's shadow and
+    extension rays together) and shading, no partitions.  Every pixel, AOV and ray count equals
+    the oracle's: single-material and all-material shading, the two-level world structure, several
+    samples per pixel, depth 7, one rank's compact tiles; "field_stages" (PUPIL_FRAME_PATHS=0) is
+    the same render through the stage pipeline."""
+    import ctypes as C
+
+    if case == "field_stages":
+        monkeypatch.setenv("PUPIL_FRAME_PATHS", "0")
+    if case == "materials_two_level":
+        monkeypatch.setenv("PUPIL_ACCEL", "two_level")
+    spp, tile = 1, (32, 0, 1)
+    if case.startswith("cornell"):
+        desc = _cornell(64, depth=7 if "depth7" in case else 4).desc()
+        spp = 3 if "spp3" in case else 1
+    elif case.startswith("materials"):
+        desc = World().load_scene(scenes.cornell_materials_xml(os.path.join(TMP, "cbmat80.xml"), 80, 80, 6)).desc()
+        spp = 2
+    else:
+        desc = scenes.sphere_field(27, 160, 96, 4, seed=5).desc()
+        tile = (16, 1, 3) if case == "field_tiles" else tile
+    gpu = render_gpu(desc, spp, tile=tile, stats=False)
+    assert gpu["stats"]["frame_launches"] == (0 if case == "field_stages" else 1)
+    pixels = None
+    if tile[2] > 1:
+        lib = abi.load_library()
+        n = C.c_uint32(0)
+        lib.pupil_pt_local_pixels(desc.width, desc.height, tile[0], tile[1], tile[2], None, C.byref(n))
+        pixels = np.zeros(n.value, np.uint32)
+        lib.pupil_pt_local_pixels(desc.width, desc.height, tile[0], tile[1], tile[2],
+                                  pixels.ctypes.data_as(abi.u32p), C.byref(n))
+    ref = oracle.OracleScene(desc).render(spp=spp, pixels=pixels)
+    assert compare(gpu, ref, f"one-launch-{case}") == len(ref["accum"])
+    assert np.array_equal(gpu["albedo"], ref["albedo"]) and np.array_equal(gpu["normal"], ref["normal"])
+    assert np.array_equal(gpu["test"], ref["test"])
+    s, rs = gpu["stats"], ref["stats"]
+    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
+        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
 
 
 def test_non_accumulating_frame_overwrites():
@@ -1058,6 +1103,7 @@ def test_shade_list_modes_parity(mode, monkeypatch):
     """Shading over the material-bin partition, or over the traced list with per-path
     bins (the default for single-material scenes), forced on a scene with all seven BSDFs."""
     monkeypatch.setenv("PUPIL_SHADE_LIST", mode)
+    monkeypatch.setenv("PUPIL_FRAME_PATHS", "0")  # shade modes of the stage pipeline
     p = scenes.cornell_materials_xml(os.path.join(TMP, "cbmat96.xml"), 96, 96, 6)
     desc = World().load_scene(p).desc()
     gpu = render_gpu(desc, 4)

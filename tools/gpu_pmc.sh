@@ -20,3 +20,17 @@ K=${PMC_KERNELS:-"k_trace4<0, false, false>|k_trace4<3, false, false>|k_trace4<4
 PUPIL_ROUND=${PUPIL_ROUND:-r03} python3 tools/pmc_summary.py gpurun_out/pmc --json "$K" gpurun_out/pmc_config$CFG.json \
   "config $CFG default bench: all non-instrumented k_trace4 launches (primary extend, mixed extension/shadow, pipelined mixed + camera rays)"
 python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt
+# the shade kernels of the same passes (per-path HBM bytes / VALU of the dominant non-traversal stage)
+SK=$(python3 - <<'PY'
+import csv, glob, re
+names = set()
+for f in glob.glob("gpurun_out/pmc/p1/*counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
+        k = re.sub(r"\(.*", "", r["Kernel_Name"].replace("void ", "").replace("pupil::(anonymous namespace)::", "").replace("pupil::", ""))
+        if k.startswith("k_shade"):
+            names.add(k)
+print("|".join(sorted(names)))
+PY
+)
+[ -n "$SK" ] && PUPIL_ROUND=${PUPIL_ROUND:-r05} python3 tools/pmc_summary.py gpurun_out/pmc --json "$SK" gpurun_out/pmc_shade_config$CFG.json \
+  "config $CFG default bench: the shade launches (per shaded path: rays_traced here counts the traversal's rays; see shade_paths)"

@@ -40,6 +40,7 @@ for step in ${STEPS:-suite smoke}; do
     CONFIG=$k bash tools/gpu_pmc.sh > $O/pmc$k.log 2>&1 || { tail -5 $O/pmc$k.log; exit 1; }
     cp gpurun_out/pmc_config$k.json $O/pmc_config$k.json
     [ "${COMMIT_PMC:-0}" = "1" ] && cp gpurun_out/pmc_config$k.json profiles/pmc_config$k.json
+    [ -f gpurun_out/pmc_shade_config$k.json ] && mv gpurun_out/pmc_shade_config$k.json $O/pmc_shade_config$k.json
     mv gpurun_out/pmc_summary.txt $O/pmc_summary$k.txt; rm -rf gpurun_out/pmc
     python3 -c "import json; d=json.load(open('$O/pmc_config$k.json')); print('pmc$k', round(d['traffic_bytes_per_ray'],1), 'B/ray', round(d['valu_insts_per_ray'],2), 'VALU/ray')" ;;
   bench4)
