@@ -13,6 +13,7 @@
 #   ab             alternating same-box A/B of builds / env (tools/gpu_lib_sweep.sh, $LIBS, $ROUNDS)
 #   probe          OnRun shard probe (tools/shard_probe.py; PROBE_ARGS)
 #   dropin         C++ drop-in cadence A/B (tools/gpu_dropin_ab.sh)
+#   pacing         C++ drop-in OnRun p50/p99/max per frame-group size + speculation waste (tools/gpu_pacing.sh)
 #   prof           rocprofv3 --kernel-trace --stats of a short default bench + the timed-launch check
 #   ranks          bench.py N-rank rehearsal over gloo on this one GPU (tools/gpu_rehearse_ranks.sh)
 #   cppranks       C++ drop-in with 2 ranks on this GPU over the host-staged test transport
@@ -57,6 +58,8 @@ for step in ${STEPS:-suite smoke}; do
     cut -c1-160 $O/probe.txt ;;
   dropin)
     bash tools/gpu_dropin_ab.sh > $O/dropin.txt 2>&1; rc=$?; cut -c1-200 $O/dropin.txt; [ $rc -eq 0 ] || exit $rc ;;
+  pacing)
+    OUT=${OUT:-gpurun_out/session} bash tools/gpu_pacing.sh > $O/pacing.log 2>&1; rc=$?; cut -c1-220 $O/pacing.log; [ $rc -eq 0 ] || exit $rc ;;
   prof)
     cd /tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 4 --cpu-baseline 0 --dropin 0 ${BENCH4_ARGS:-} > $O/prof.log 2>&1
