@@ -11,10 +11,9 @@
 namespace pupil {
 
 constexpr int kTraceBlock = 128;
-#ifndef PUPIL_W4_WAVES  // r05 A/B (8 waves)
-#define PUPIL_W4_WAVES 7
-#endif
-constexpr int kTraceWavesPerSimd = PUPIL_W4_WAVES;  // persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8 waves at <= 64 VGPRs: 11 % slower, r03 A/B)
+// persistent BVH4 kernels: occupancy target (<= 72 VGPRs; 6 waves: 3 % slower, 8 waves at <= 64 VGPRs:
+// 8-11 % slower, r03 / r05 A/B, profiles/r05_stack_ab.txt)
+constexpr int kTraceWavesPerSimd = 7;
 constexpr int kTraceWavesPerSimdTL = 5;  // two-level variant (<= 96 VGPRs; A/B r02 on config 5: 4 waves 688, 5: 743, 6: 716 Mrays/s)
 constexpr int kStackOvf = 160;  // per-thread global overflow entries
 constexpr int kRing = 16;       // persistent BVH4 kernels: per-lane LDS ring entries (spills to the overflow column)
