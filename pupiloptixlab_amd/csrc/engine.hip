@@ -468,6 +468,15 @@ uint64_t nodes4_count(const pupil_pt *pt) {
 int refresh_node_bound(pupil_pt *pt) {
     pt->sc.node_bound[0] = pt->sc.node_bound[1] = pt->sc.node_bound[2] = 0.f;
     const uint64_t n = nodes4_count(pt);
+    {  // LDS-resident top of the tree (pt_scene.h top_nodes); two-level: within the TLAS
+        static const uint32_t want = [] {
+            const char *e = std::getenv("PUPIL_TOP_NODES");
+            return e ? (uint32_t)std::min<long>(kTopNodes, std::max(0L, std::atol(e))) : kTopNodes;
+        }();
+        uint64_t live = pt->sc.nodes4 ? n : 0;
+        if (pt->two_level) live = std::min<uint64_t>(live, pt->tl.tlas_nodes);
+        pt->sc.top_nodes = (uint32_t)std::min<uint64_t>(want, live);
+    }
     if (!pt->sc.nodes4 || n == 0) return PUPIL_OK;
     if (pt->two_level) {
         const uint64_t tlas = std::min<uint64_t>(pt->tl.tlas_nodes, n), cap = std::min<uint64_t>(pt->tl.tlas_cap, n);

@@ -108,6 +108,10 @@ struct alignas(64) Bvh4Node {
     float sy, sz;       // scales of the y and z planes
 };
 constexpr int kEmptyLink = 0x7FFFFFFF;
+// BVH4 nodes the flat traversal keeps in LDS: the root, its 4 children and the first 11 of
+// the third level of the breadth-first layout; 1 KB per 128-lane block keeps 14 blocks (7
+// waves per SIMD) within the CU's 160 KB of LDS in 512-B allocation granules
+constexpr uint32_t kTopNodes = 16;
 // Largest BVH4 node array: the traversal addresses nodes by 32-bit byte offsets.
 constexpr uint64_t kMaxNodes4 = 1ull << 26;
 // Traversal terminator (stack bottom); also the root link of an empty scene.
@@ -143,6 +147,10 @@ struct DeviceScene {
     uint32_t trace_refill;  // BVH4 kernels: refill a wave's idle lanes once this many are idle
     uint32_t num_cus;       // compute units of the device (persistent grid size)
     uint32_t trace_node_min;  // BVH4 kernels: node phase ends when fewer lanes need a node
+    // nodes [0, top_nodes) are copied into each traversal block's LDS at launch and read from
+    // there (the collapse emits the BVH4 breadth first: the root and the levels below it,
+    // which every ray visits); <= kTopNodes, 0 = off (refresh_node_bound)
+    uint32_t top_nodes;
     // per axis, max over every BVH4 node of |o| + 512 s (launch_node_bound after each build
     // and refit): the slab test's rounding bound is then one value per ray (pt_traverse.h
     // slab_error) instead of one per node visit

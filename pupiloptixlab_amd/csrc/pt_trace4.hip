@@ -46,8 +46,16 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
 template <int MODE, bool ANY, bool STATS, bool TL>
 __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathState &ps, const Queues &q,
                                             const TraceJob &job, int *ovf, uint32_t ovf_threads,
-                                            const TraceStats &stats, int *s_ring, float *s_aux, float *s_tst) {
+                                            const TraceStats &stats, int *s_ring, float *s_aux, float *s_tst,
+                                            Bvh4Node *s_top) {
     constexpr float kInf = __builtin_huge_valf();
+    // the top of the tree (nodes [0, top), breadth first) into LDS: every ray starts there
+    const uint32_t top = TL ? 0u : sc.top_nodes;
+    if (!TL) {
+        for (uint32_t i = threadIdx.x; i < top * 4u; i += kTraceBlock)
+            reinterpret_cast<float4 *>(s_top)[i] = reinterpret_cast<const float4 *>(sc.nodes4)[i];
+        __syncthreads();
+    }
     constexpr bool kMixed = MODE == kModeMixed || MODE == kModeMixedAhead;
     const uint32_t n_next = kMixed ? q.counts[kCntNext] : 0u;
     // mixed launches may carry the next render's camera rays (render-ahead, TraceJob::ahead_off)
@@ -221,7 +229,9 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         // ---- traverse until this lane's ray terminates or it needs a leaf while others do too
         if (active) {
             while ((uint32_t)node < (uint32_t)kSentinel) {
-                const Bvh4Node n = load_node4(sc, node);
+                Bvh4Node n;
+                if ((uint32_t)node < top) n = s_top[node];
+                else n = load_node4(sc, node);
                 if (STATS) {
                     if (kMixed && any) nv_sh++;
                     else nv++;
@@ -420,7 +430,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     __shared__ int s_ring[kRing * kTraceBlock];
     __shared__ float s_aux[4 * kTraceBlock];
     __shared__ float s_tst[STATS ? kRing * kTraceBlock : 1];
-    trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst);
+    __shared__ Bvh4Node s_top[kTopNodes];
+    trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst, s_top);
 }
 
 // two-level variant: 9 more live registers (object-space box ray, margin,
@@ -431,7 +442,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTr
     __shared__ int s_ring[kRing * kTraceBlock];
     __shared__ float s_aux[4 * kTraceBlock];
     __shared__ float s_tst[STATS ? kRing * kTraceBlock : 1];
-    trace4_body<MODE, ANY, STATS, true>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst);
+    trace4_body<MODE, ANY, STATS, true>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst, nullptr);
 }
 
 
