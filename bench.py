@@ -522,6 +522,16 @@ def roofline(args, st_bytes, timed):
                                    # the same issue rate against the 2.4 GHz spec clock (MI355X_MICROARCH.md)
                                    "frac_at_spec_clock": round(need / sec / 1e9 / (simds * SPEC_CLOCK_GHZ), 4),
                                    "valu_insts_per_ray": round(pmc["valu_insts_per_ray"], 2)}
+        if pmc.get("ta_busy_cycles_per_ray") and pmc.get("clock_ghz"):
+            # the vector-memory address unit (one TA per CU) processes every VMEM wave-instruction
+            # (node and record gathers, ray loads); r05 counters put it at 0.77 busy
+            need = pmc["ta_busy_cycles_per_ray"] * rays_launch
+            cands["ta-busy"] = {"achieved": need / sec / 1e9, "peak": 256 * pmc["clock_ghz"],
+                                "unit": "G TA-cycles/s",
+                                "how": "PMC TA_TA_BUSY_sum per traced ray x rays per launch / HIP-event launch time, "
+                                       "over 256 TAs (one per CU) at the GRBM-measured clock",
+                                "frac_at_spec_clock": round(need / sec / 1e9 / (256 * SPEC_CLOCK_GHZ), 4),
+                                "vmem_insts_per_ray": round(pmc.get("vmem_insts_per_ray") or 0.0, 2)}
     for c in cands.values():
         c["frac"] = round(c["achieved"] / c["peak"], 4)
         c["achieved"] = round(c["achieved"], 2)

@@ -93,6 +93,11 @@ def traffic_json(root, kernels, out_path, note=""):
            "rays_traced": n_rays,
            "traffic_bytes_per_ray": (2.0 * total("FETCH_SIZE") + total("WRITE_SIZE")) * 1024.0 / n_rays if n_rays else None,
            "valu_insts_per_ray": total("SQ_INSTS_VALU") / n_rays if n_rays and valu else None,
+           # vector-memory address processing: TA busy cycles summed over the 256 CUs' TAs, and the
+           # VMEM wave-instructions they processed (r05: the traversal's binding unit)
+           "ta_busy_cycles_per_ray": total("TA_TA_BUSY_sum") / n_rays if n_rays and pooled("TA_TA_BUSY_sum") else None,
+           "vmem_insts_per_ray": total("TA_TOTAL_WAVEFRONTS_sum") / n_rays
+           if n_rays and pooled("TA_TOTAL_WAVEFRONTS_sum") else None,
            "dispatches": len(d),
            "simd_efficiency": simd,
            "note": note}
