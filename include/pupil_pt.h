@@ -305,10 +305,6 @@ typedef struct pupil_pt_counters {
     /* renders run as one persistent launch per frame (renders that start no frame ahead and
      * have at most PUPIL_FRAME_PATHS paths: the moving-camera OnRun, one rank's tiles) */
     uint64_t frame_launches;
-    /* 48-B slots of the traversal layout the flat and world-mode kernels walk (nodes and leaf
-     * records, csrc/bvh48.hip); 0 when the 64-B kernels run (object-mode two-level scenes,
-     * leaves of 8 records, PUPIL_NODE48=0) */
-    uint64_t traversal_slots48;
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;

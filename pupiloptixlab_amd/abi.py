@@ -97,8 +97,7 @@ class Counters(C.Structure):
                 # ABI 5
                 ("node_loop_iters", C.c_uint64), ("node_loop_lanes", C.c_uint64), ("leaf_loop_iters", C.c_uint64),
                 ("leaf_loop_lanes", C.c_uint64), ("refills", C.c_uint64), ("refill_lanes", C.c_uint64),
-                ("frame_launches", C.c_uint64),
-                ("traversal_slots48", C.c_uint64)]
+                ("frame_launches", C.c_uint64)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_ if name != "pad_counters"}

@@ -171,7 +171,6 @@ struct pupil_pt {
     unsigned long long *ray_cum = nullptr;
     bool snap_taken = false;
     uint32_t *node_bound = nullptr;                // launch_node_bound's result (3 floats as bits)
-    Trav48 t48;                                    // the 48-B traversal layout (bvh48.hip), rebuilt with node_bound
     uint64_t primary_cum = 0;                      // host running total of camera rays
     uint32_t last_paths = 0, last_iters = 0;
     uint64_t last_primary = 0;
@@ -251,7 +250,6 @@ struct pupil_pt {
         for (void *p : allocs) (void)hipFree(p);
         free_lbvh(bvh);
         free_two_level(tl);
-        free_trav48(t48);
         if (pixel_map) (void)hipFree(pixel_map);
         for (auto e : trace_events) (void)hipEventDestroy(e);
         if (ev_begin) (void)hipEventDestroy(ev_begin);
@@ -467,30 +465,6 @@ uint64_t nodes4_count(const pupil_pt *pt) {
 // one 12-B read back, the traversal kernels take it by value).  Live nodes only: in the
 // two-level layouts the TLAS reserve [tlas_nodes, tlas_cap) is never written, and
 // whatever an earlier allocation left there must not loosen the bound of every ray.
-// The 48-B traversal layout (bvh48.hip) of the current flat / world-mode BVH4, rebuilt after
-// every build and refit (its nodes copy the 64-B nodes' boxes); object-mode two-level scenes
-// and trees it cannot hold (leaves of 8 records, PUPIL_NODE48=0) keep the 64-B kernels
-// (sc.t48 = null).
-int refresh_trav48(pupil_pt *pt) {
-    const char *env = std::getenv("PUPIL_NODE48");  // read per build: tests compare both layouts in one process
-    const bool want = !env || std::atoi(env) != 0;
-    pt->sc.t48 = nullptr;
-    pt->sc.root48 = (uint32_t)kTraverseDone;
-    if (!pt->two_level) pt->sc.attrs = pt->bvh.attrs;  // flat hits name 64-B record slots unless t48 runs
-    if (!want || (pt->two_level && !pt->tl.world) || !pt->sc.nodes4) return PUPIL_OK;
-    // flat hits name their 48-B slot, so the shading records follow; world-mode hits name the
-    // global primitive id
-    const float4 *attrs = pt->two_level ? nullptr : pt->bvh.attrs;
-    const int rc = build_trav48(pt->sc.nodes4, nodes4_count(pt), pt->sc.root_link4, pt->sc.prims, pt->num_prims,
-                                attrs, pt->t48, pt->own_stream);
-    if (rc == PUPIL_ERR_UNSUPPORTED) return PUPIL_OK;
-    if (rc != PUPIL_OK) return fail(rc, "48-B traversal layout build failed");
-    pt->sc.t48 = pt->t48.slots;
-    pt->sc.root48 = pt->t48.root;
-    if (attrs) pt->sc.attrs = pt->t48.attrs;
-    return PUPIL_OK;
-}
-
 int refresh_node_bound(pupil_pt *pt) {
     pt->sc.node_bound[0] = pt->sc.node_bound[1] = pt->sc.node_bound[2] = 0.f;
     const uint64_t n = nodes4_count(pt);
@@ -503,7 +477,7 @@ int refresh_node_bound(pupil_pt *pt) {
         if (pt->two_level) live = std::min<uint64_t>(live, pt->tl.tlas_nodes);
         pt->sc.top_nodes = (uint32_t)std::min<uint64_t>(want, live);
     }
-    if (!pt->sc.nodes4 || n == 0) return refresh_trav48(pt);
+    if (!pt->sc.nodes4 || n == 0) return PUPIL_OK;
     if (pt->two_level) {
         const uint64_t tlas = std::min<uint64_t>(pt->tl.tlas_nodes, n), cap = std::min<uint64_t>(pt->tl.tlas_cap, n);
         launch_node_bound(pt->sc.nodes4, tlas, pt->node_bound, pt->own_stream, true);
@@ -515,7 +489,7 @@ int refresh_node_bound(pupil_pt *pt) {
     HIP_TRY(hipMemcpyAsync(b, pt->node_bound, sizeof(b), hipMemcpyDeviceToHost, pt->own_stream));
     HIP_TRY(hipStreamSynchronize(pt->own_stream));
     for (int a = 0; a < 3; a++) std::memcpy(&pt->sc.node_bound[a], &b[a], 4);
-    return refresh_trav48(pt);
+    return PUPIL_OK;
 }
 
 // Local pixel list of a rank: tiles t with t % world == rank, row-major tile
@@ -1387,7 +1361,6 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
     c.ring_budget_bytes = (uint64_t)pt->pipe_budget;
     c.accel_refits = pt->refits;
     c.frame_launches = pt->frame_launches;
-    c.traversal_slots48 = pt->sc.t48 ? pt->t48.used : 0u;
     for (int a = 0; a < 3; a++) c.node_bound[a] = pt->sc.node_bound[a];
     if (pt->last_paths) {
         // rays traced by the last render's launches (pipelined renders: of every frame in

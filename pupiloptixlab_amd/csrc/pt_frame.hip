@@ -50,9 +50,8 @@ struct FrameJob {
 };
 
 // material bin of a hit record slot (flat / world-mode records: trace4_body's retire)
-template <bool N48>
 __device__ __forceinline__ uint32_t record_bin(const DeviceScene &sc, uint32_t best_idx) {
-    const uint32_t mt = __float_as_uint(N48 ? sc.t48[kSlot48F4 * best_idx + 2].w : sc.prims[kRecF4 * best_idx + 2].w);
+    const uint32_t mt = __float_as_uint(sc.prims[kRecF4 * best_idx + 2].w);
     return (mt >= 1u && mt <= 7u) ? mt : 8u;
 }
 
@@ -99,7 +98,7 @@ struct WaveQueue {
     }
 };
 
-template <uint32_t MAT, bool N48>
+template <uint32_t MAT>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_frame(
     DeviceScene sc, FrameParams fp, PathState ps, FrameJob job, int *ovf, uint32_t ovf_threads) {
     constexpr float kInf = __builtin_huge_valf();
@@ -145,10 +144,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4))
         b1 = b2 = 0.f;
         found = false;
         st.reset();
-        node = N48 ? (int)sc.root48 : (int)sc.root_link4;
+        node = (int)sc.root_link4;
         leaf = 0;
         be = slab_errors(r.o, r.idir, sc.node_bound);
-        if (N48 ? is_leaf48(node) : node < 0) {
+        if (node < 0) {
             leaf = node;
             node = kSentinel;
         }
@@ -233,23 +232,20 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4))
         if (!__any(active)) continue;  // the shade above, or another dequeue
         // ---- traverse (trace4_body's while-while loops, flat BVH4)
         if (active) {
-            while (N48 ? is_node48(node) : (uint32_t)node < (uint32_t)kSentinel) {
+            while ((uint32_t)node < (uint32_t)kSentinel) {
+                const Bvh4Node n = load_node4(sc, node);
                 float t[4];
                 int l[4];
-                if (N48) {
-                    visit48(load_node48(sc.t48, node48_offset(node)), r.o, r.idir, be, tmin, tmax, t, l);
-                } else {
-                    visit4(load_node4(sc, node), r.o, r.idir, be, tmin, tmax, t, l);
-                }
+                visit4(n, r.o, r.idir, be, tmin, tmax, t, l);
                 if (t[0] == kInf) {
                     node = st.pop();
                 } else {
                     node = l[0];
                     st.reserve3();
                     st.push3(l[1], l[2], l[3], t[1] != kInf, t[2] != kInf, t[3] != kInf);
-                    if (!N48 && node == kEmptyLink) node = st.pop();
+                    if (node == kEmptyLink) node = st.pop();
                 }
-                if ((N48 ? is_leaf48(node) : node < 0) && leaf >= 0) {
+                if (node < 0 && leaf >= 0) {
                     leaf = node;
                     node = st.pop();
                 }
@@ -257,18 +253,11 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4))
             }
             while (leaf < 0) {
                 uint32_t np_cnt = 0;
-                if (N48 ? intersect_leaf_dyn<false, decltype(ray_dir), true>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, np_cnt, found,
-                                                  any, ray_dir)
-                        : intersect_leaf_dyn<false>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, np_cnt, found,
-                                                    any, ray_dir))
+                if (intersect_leaf_dyn<false>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, np_cnt, found, any,
+                                              ray_dir))
                     break;
-                if (N48) {
-                    leaf = is_leaf48(node) ? node : 0;
-                    if (leaf < 0) node = st.pop();
-                } else {
-                    leaf = node;
-                    if (node < 0) node = st.pop();
-                }
+                leaf = node;
+                if (node < 0) node = st.pop();
             }
         }
         const bool done = active && ((node == kSentinel && leaf >= 0) || (any && found));
@@ -276,7 +265,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4))
         if (done && !any) {  // extension / camera ray: the hit record, then the path waits for its shade
             const uint32_t hidx = sc.two_level ? best_key : best_idx;
             st_ps(ps.hit + p, make_float4(found ? tmax : -1.f, b1, b2, __uint_as_float(found ? hidx : kMissIndex)));
-            if (!sc.single_bin) ps.mbin[p] = (uint8_t)(found ? record_bin<N48>(sc, best_idx) : 0u);
+            if (!sc.single_bin) ps.mbin[p] = (uint8_t)(found ? record_bin(sc, best_idx) : 0u);
         }
         if (done && any && !found) {  // main.cu:124-139
             const float4 c = ld_ps(ps.sh_c + p);
@@ -321,20 +310,14 @@ void launch_frame(const DeviceScene &sc, const FrameParams &fp, const PathState 
     const uint32_t resident = sc.num_cus * 4u * 4u / kFrameWaves;
     const uint32_t by_paths = (fp.num_paths + kTraceBlock - 1) / kTraceBlock;
     const uint32_t blocks = std::min(ovf_threads / kTraceBlock, std::max(1u, std::min(resident, by_paths)));
-    const bool n48 = sc.t48 != nullptr;
-    if (sc.single_bin == PUPIL_MAT_DIFFUSE) {
-        if (n48)
-            hipLaunchKernelGGL((k_frame<PUPIL_MAT_DIFFUSE, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, fp, ps, job,
-                               ovf, ovf_threads);
-        else
-            hipLaunchKernelGGL((k_frame<PUPIL_MAT_DIFFUSE, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, fp, ps,
-                               job, ovf, ovf_threads);
-    } else if (n48) {
-        hipLaunchKernelGGL((k_frame<0xFFu, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, fp, ps, job, ovf,
+    switch (sc.single_bin) {
+    case PUPIL_MAT_DIFFUSE:
+        hipLaunchKernelGGL(k_frame<PUPIL_MAT_DIFFUSE>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, fp, ps, job, ovf,
                            ovf_threads);
-    } else {
-        hipLaunchKernelGGL((k_frame<0xFFu, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, fp, ps, job, ovf,
-                           ovf_threads);
+        break;
+    default:
+        hipLaunchKernelGGL(k_frame<0xFFu>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, fp, ps, job, ovf, ovf_threads);
+        break;
     }
 }
 

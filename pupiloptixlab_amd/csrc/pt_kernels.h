@@ -185,13 +185,6 @@ void launch_frame(const DeviceScene &sc, const FrameParams &fp, const PathState 
 // per axis max of |o| + 512 s over n BVH4 nodes into out[0..2] (float bits; clear: out is
 // zeroed first, else the max also covers what it holds), the bound DeviceScene::node_bound holds
 void launch_node_bound(const Bvh4Node *nodes, uint64_t n, uint32_t *out, hipStream_t s, bool clear = true);
-// The 48-B traversal layout (bvh48.hip) of a flat or world-mode BVH4: rebuilt from the 64-B
-// nodes and record slots after every build and refit.  PUPIL_OK, or PUPIL_ERR_UNSUPPORTED when
-// the tree does not fit it (a leaf of 8 records, > 44 M slots): the 64-B kernels run then.
-// attrs (flat scenes; null otherwise): the shading records, scattered to Trav48::attrs by slot.
-int build_trav48(const Bvh4Node *nodes, uint64_t num_nodes, uint32_t root_link, const float4 *prims,
-                 uint64_t num_slots64, const float4 *attrs, Trav48 &out, hipStream_t s);
-void free_trav48(Trav48 &t);
 void launch_accumulate(const FrameParams &fp, const PathState &ps, const float *aov_src, bool clear_flags,
                        hipStream_t s);
 uint32_t trace_grid_blocks();

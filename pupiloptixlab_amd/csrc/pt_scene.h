@@ -138,28 +138,8 @@ struct Camera {
     float c2w[16];  // camera_to_world
 };
 
-// 48-B traversal slots (bvh48.hip): nodes and leaf records of the flat / world-mode BVH4 in
-// one array, each node's children one contiguous block.  Links into it keep the 64-B layout's
-// sign convention -- negative, ~((slot << 3) | code) -- with code 7 = internal node at `slot`,
-// code c < 7 = leaf of c + 1 records from `slot` (so leaves hold at most 7 primitives).
-#ifndef PUPIL_SLOT_F4
-#define PUPIL_SLOT_F4 3
-#endif
-constexpr uint32_t kSlot48F4 = PUPIL_SLOT_F4;  // float4 per 48-B slot
-constexpr uint32_t kCode48Node = 7u;
-struct Trav48 {
-    float4 *slots = nullptr;
-    float4 *attrs = nullptr;               // flat scenes: shading records by 48-B slot (kAttrStride float4 each)
-    uint64_t cap = 0;                      // slots allocated
-    uint64_t used = 0;                     // slots written
-    uint32_t root = (uint32_t)kTraverseDone;  // link of the root (kTraverseDone: empty scene)
-};
-
 struct DeviceScene {
     const Bvh4Node *nodes4;
-    // the 48-B traversal layout of nodes4 / prims (null: the 64-B kernels run); root48 its root link
-    const float4 *t48;
-    uint32_t root48;
     const float4 *prims;  // kRecF4 float4 per record slot, leaf order (holes between leaves)
     const float4 *attrs;  // kAttrStride float4 per primitive, same order (hit reconstruction)
     uint32_t num_prims;

@@ -43,27 +43,19 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
 // instance each; entering one pushes the pending TLAS link and kReturnLink and
 // switches the box tests to the instance's object-space ray; popping
 // kReturnLink switches back.  Spheres are tested at their TLAS leaf.
-// N48: the 48-B layout (bvh48.hip, DeviceScene::t48): links ~((slot << 3) | code), internal iff
-// negative with code 0 bits (is_node48), leaves keep the 64-B layout's encoding
-template <int MODE, bool ANY, bool STATS, bool TL, bool N48 = false>
+template <int MODE, bool ANY, bool STATS, bool TL>
 __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathState &ps, const Queues &q,
                                             const TraceJob &job, int *ovf, uint32_t ovf_threads,
                                             const TraceStats &stats, int *s_ring, float *s_aux, float *s_tst,
                                             Bvh4Node *s_top) {
     constexpr float kInf = __builtin_huge_valf();
-    // the top of the tree (nodes [0, top), breadth first; 48-B layout: the first slots, the root
-    // and its block) into LDS: every ray starts there
+    // the top of the tree (nodes [0, top), breadth first) into LDS: every ray starts there
     const uint32_t top = TL ? 0u : sc.top_nodes;
-    // N48: the whole slots among the copied bytes
-    const uint32_t top_bytes = top * (uint32_t)sizeof(Bvh4Node) / (kSlot48F4 * 16u) * (kSlot48F4 * 16u);
     if (!TL) {
-        const float4 *src = N48 ? sc.t48 : reinterpret_cast<const float4 *>(sc.nodes4);
-        for (uint32_t i = threadIdx.x; i < top * 4u; i += kTraceBlock) reinterpret_cast<float4 *>(s_top)[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < top * 4u; i += kTraceBlock)
+            reinterpret_cast<float4 *>(s_top)[i] = reinterpret_cast<const float4 *>(sc.nodes4)[i];
         __syncthreads();
     }
-    // link predicates of the layout: an internal node / a leaf
-    auto internal = [](int l) { return N48 ? is_node48(l) : (uint32_t)l < (uint32_t)kSentinel; };
-    auto is_leaf = [](int l) { return N48 ? is_leaf48(l) : l < 0; };
     constexpr bool kMixed = MODE == kModeMixed || MODE == kModeMixedAhead;
     const uint32_t n_next = kMixed ? q.counts[kCntNext] : 0u;
     // mixed launches may carry the next render's camera rays (render-ahead, TraceJob::ahead_off)
@@ -213,7 +205,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     b1 = b2 = 0.f;
                     found = false;
                     st.reset();
-                    node = N48 ? (int)sc.root48 : (int)sc.root_link4;
+                    node = (int)sc.root_link4;
                     leaf = 0;
                     be = slab_errors(r.o, r.idir, sc.node_bound);
                     if (TL) {
@@ -221,7 +213,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         bo = r.o;
                         bi = r.idir;
                     }
-                    if (is_leaf(node)) {
+                    if (node < 0) {
                         leaf = node;
                         node = kSentinel;
                     }
@@ -236,18 +228,10 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         }
         // ---- traverse until this lane's ray terminates or it needs a leaf while others do too
         if (active) {
-            while (internal(node)) {
+            while ((uint32_t)node < (uint32_t)kSentinel) {
                 Bvh4Node n;
-                Node48 n48;
-                if (N48) {
-                    const uint32_t off = node48_offset(node);
-                    if (off < top_bytes) n48 = load_node48(reinterpret_cast<const float4 *>(s_top), off);
-                    else n48 = load_node48(sc.t48, off);
-                } else if ((uint32_t)node < top) {
-                    n = s_top[node];
-                } else {
-                    n = load_node4(sc, node);
-                }
+                if ((uint32_t)node < top) n = s_top[node];
+                else n = load_node4(sc, node);
                 if (STATS) {
                     if (kMixed && any) nv_sh++;
                     else nv++;
@@ -267,8 +251,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 }
                 float t[4];
                 int l[4];
-                if (N48) visit48(n48, r.o, r.idir, be, tmin, tmax, t, l);
-                else if (TL) visit4(n, bo, bi, be, tmin, tmax, t, l);
+                if (TL) visit4(n, bo, bi, be, tmin, tmax, t, l);
                 else visit4(n, r.o, r.idir, be, tmin, tmax, t, l);
                 if (STATS) {
                     n_cullable += t_node > tmax ? 1u : 0u;
@@ -283,9 +266,9 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     st.reserve3();
                     st.push3t(t[1], t[2], t[3], t[2] != kInf, t[3] != kInf);
                     st.push3(l[1], l[2], l[3], t[1] != kInf, t[2] != kInf, t[3] != kInf);
-                    if (!N48 && node == kEmptyLink) node = st.pop();  // degenerate child boxes only (LinStack)
+                    if (node == kEmptyLink) node = st.pop();  // degenerate child boxes only (LinStack)
                 }
-                if (is_leaf(node) && leaf >= 0) {  // postpone the leaf, keep descending
+                if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
                     leaf = node;
                     node = st.pop();
                     if (STATS) t_node = st.tpop;
@@ -339,20 +322,12 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     if (intersect_leaf_tl<STATS>(sc, r, leaf, inst, tmin, tmax, best_key, best_idx, b1, b2,
                                                  np_cnt, found, any))
                         break;
-                } else if (N48 ? intersect_leaf_dyn<STATS, decltype(ray_dir), true>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2, np_cnt,
-                                                         found, any, ray_dir)
-                               : intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2,
-                                                           np_cnt, found, any, ray_dir)) {
+                } else if (intersect_leaf_dyn<STATS>(sc, r, leaf, tmin, tmax, best_key, best_idx, b1, b2,
+                                                     np_cnt, found, any, ray_dir)) {
                     break;
                 }
-                // the lane's other pending link: a second leaf (popped past), else back to the nodes
-                if (N48) {
-                    leaf = is_leaf48(node) ? node : 0;
-                    if (leaf < 0) node = st.pop();
-                } else {
-                    leaf = node;
-                    if (node < 0) node = st.pop();
-                }
+                leaf = node;
+                if (node < 0) node = st.pop();
             }
             if (TL && node == kReturnLink && leaf >= 0 && !(any && found)) {  // BLAS exhausted: back to the TLAS
                 in_blas = false;
@@ -381,8 +356,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     if (TL) {
                         bin = sc.instances[sc.prim_inst[best_idx]].bin;
                     } else {
-                        const uint32_t mt = __float_as_uint(
-                            N48 ? sc.t48[kSlot48F4 * best_idx + 2].w : sc.prims[kRecF4 * best_idx + 2].w);
+                        const uint32_t mt = __float_as_uint(sc.prims[kRecF4 * best_idx + 2].w);
                         bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
                     }
                 }
@@ -450,14 +424,14 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     }
 }
 
-template <int MODE, bool ANY, bool STATS, bool N48>
+template <int MODE, bool ANY, bool STATS>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4(
     DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
     __shared__ int s_ring[kRing * kTraceBlock];
     __shared__ float s_aux[4 * kTraceBlock];
     __shared__ float s_tst[STATS ? kRing * kTraceBlock : 1];
     __shared__ Bvh4Node s_top[kTopNodes];
-    trace4_body<MODE, ANY, STATS, false, N48>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst, s_top);
+    trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst, s_top);
 }
 
 // two-level variant: 9 more live registers (object-space box ray, margin,
@@ -501,19 +475,12 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
         else
             hipLaunchKernelGGL((k_trace4tl<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
                                ovf, ovf_threads, st);
-    } else if (sc.t48) {
-        if (stats)
-            hipLaunchKernelGGL((k_trace4<MODE, ANY, true, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
-                               ovf, ovf_threads, st);
-        else
-            hipLaunchKernelGGL((k_trace4<MODE, ANY, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
-                               ovf, ovf_threads, st);
     } else if (stats) {
-        hipLaunchKernelGGL((k_trace4<MODE, ANY, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
-                           ovf, ovf_threads, st);
+        hipLaunchKernelGGL((k_trace4<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
+                           ovf_threads, st);
     } else {
-        hipLaunchKernelGGL((k_trace4<MODE, ANY, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
-                           ovf, ovf_threads, st);
+        hipLaunchKernelGGL((k_trace4<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
+                           ovf_threads, st);
     }
 }
 

@@ -23,21 +23,17 @@ __device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, 
 // hit (shadow ray); a compile-time constant except in the mixed persistent kernel.
 // dirf(): the ray direction, for sphere records only (the traversal may reload it instead of
 // keeping it live)
-// N48: records in the 48-B traversal layout (DeviceScene::t48, three float4 per slot), the hit
-// index its slot
-template <bool STATS, typename DirF, bool N48 = false>
+template <bool STATS, typename DirF>
 __device__ __forceinline__ bool intersect_leaf_dyn(const DeviceScene &sc, const RayPre &r, int leaf, float tmin,
                                                    float &tmax, uint32_t &best_key, uint32_t &best_idx, float &bb1,
                                                    float &bb2, uint32_t &prims_tested, bool &found, bool any,
                                                    DirF dirf) {
     const uint32_t first = leaf_first(leaf);
     const uint32_t count = leaf_count(leaf);
-    const float4 *recs = N48 ? sc.t48 : sc.prims;
-    constexpr uint32_t kStride = N48 ? kSlot48F4 : kRecF4;
     for (uint32_t i = first; i < first + count; i++) {
-        const float4 a = recs[kStride * i + 0];
-        const float4 b = recs[kStride * i + 1];
-        const float4 c = recs[kStride * i + 2];
+        const float4 a = sc.prims[kRecF4 * i + 0];
+        const float4 b = sc.prims[kRecF4 * i + 1];
+        const float4 c = sc.prims[kRecF4 * i + 2];
         // the whole 48-B record in one round trip: without this the compiler sinks the
         // vertex loads below the sphere-bit branch, a second dependent fetch per record
         asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(c.x),
@@ -296,17 +292,15 @@ __device__ __forceinline__ vec3 slab_errors(vec3 o, vec3 idir, const float bound
     return v3(slab_error(o.x, idir.x, bound[0]), slab_error(o.y, idir.y, bound[1]), slab_error(o.z, idir.z, bound[2]));
 }
 
-// The box test of one quantized BVH4 node from its decoded fields (both layouts).
-__device__ __forceinline__ void visit_q(float ox, float oy, float oz, float sx, float sy, float sz, uint32_t qlo_x,
-                                       uint32_t qlo_y, uint32_t qlo_z, uint32_t qhi_x, uint32_t qhi_y, uint32_t qhi_z,
-                                       vec3 ro, vec3 ridir, vec3 e, float tmin, float tmax, float t[4]) {
+__device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, vec3 e, float tmin, float tmax,
+                                       float t[4], int l[4]) {
     constexpr float kInf = __builtin_huge_valf();
     const bool px = ridir.x >= 0.f, py = ridir.y >= 0.f, pz = ridir.z >= 0.f;
-    const uint32_t nx = px ? qlo_x : qhi_x, fx = px ? qhi_x : qlo_x;
-    const uint32_t ny = py ? qlo_y : qhi_y, fy = py ? qhi_y : qlo_y;
-    const uint32_t nz = pz ? qlo_z : qhi_z, fz = pz ? qhi_z : qlo_z;
-    const float ax = ox - ro.x, ay = oy - ro.y, az = oz - ro.z;
-    const float bx = sx * ridir.x, by = sy * ridir.y, bz = sz * ridir.z;
+    const uint32_t nx = px ? n.qlo_x : n.qhi_x, fx = px ? n.qhi_x : n.qlo_x;
+    const uint32_t ny = py ? n.qlo_y : n.qhi_y, fy = py ? n.qhi_y : n.qlo_y;
+    const uint32_t nz = pz ? n.qlo_z : n.qhi_z, fz = pz ? n.qhi_z : n.qlo_z;
+    const float ax = n.ox - ro.x, ay = n.oy - ro.y, az = n.oz - ro.z;
+    const float bx = n.sx * ridir.x, by = n.sy * ridir.y, bz = n.sz * ridir.z;
     const float nearx = __builtin_fmaf(ax, ridir.x, -e.x), farx = __builtin_fmaf(ax, ridir.x, e.x);
     const float neary = __builtin_fmaf(ay, ridir.y, -e.y), fary = __builtin_fmaf(ay, ridir.y, e.y);
     const float nearz = __builtin_fmaf(az, ridir.z, -e.z), farz = __builtin_fmaf(az, ridir.z, e.z);
@@ -318,56 +312,15 @@ __device__ __forceinline__ void visit_q(float ox, float oy, float oz, float sx, 
         const float tf = fminf(fminf(fminf(__builtin_fmaf(ubyte(fx, k), bx, farx), __builtin_fmaf(ubyte(fy, k), by, fary)),
                                      __builtin_fmaf(ubyte(fz, k), bz, farz)),
                                tmax);
+        l[k] = n.child[k];
         t[k] = tn <= tf ? tn : kInf;  // an empty slot (planes 255 / 0) passes only for degenerate boxes: LinStack
     }
-}
-
-__device__ __forceinline__ void sort4(float t[4], int l[4]) {
     csel(t[0], l[0], t[1], l[1]);
     csel(t[2], l[2], t[3], l[3]);
     csel(t[0], l[0], t[2], l[2]);
     csel(t[1], l[1], t[3], l[3]);
     csel(t[1], l[1], t[2], l[2]);
 }
-
-__device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, vec3 e, float tmin, float tmax,
-                                       float t[4], int l[4]) {
-    visit_q(n.ox, n.oy, n.oz, n.sx, n.sy, n.sz, n.qlo_x, n.qlo_y, n.qlo_z, n.qhi_x, n.qhi_y, n.qhi_z, ro, ridir, e,
-            tmin, tmax, t);
-#pragma unroll
-    for (int k = 0; k < 4; k++) l[k] = n.child[k];
-    sort4(t, l);
-}
-
-// ---- the 48-B layout (bvh48.hip): a node is three float4, links ~((slot << 3) | code)
-struct Node48 {
-    float4 a, b, c;
-};
-__device__ __forceinline__ uint32_t fu(float v) { return __float_as_uint(v); }
-__device__ __forceinline__ bool is_node48(int link) { return link < 0 && (link & 7) == 0; }
-__device__ __forceinline__ bool is_leaf48(int link) { return link < 0 && (link & 7) != 0; }
-// byte offset of the slot an internal link names: (slot << 3) * 6
-__device__ __forceinline__ uint32_t node48_offset(int link) { return ((uint32_t)~link & ~7u) * (2u * kSlot48F4); }
-__device__ __forceinline__ Node48 load_node48(const float4 *t48, uint32_t off) {
-    const float4 *q = reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(t48) + off);
-    return Node48{q[0], q[1], q[2]};
-}
-__device__ __forceinline__ void visit48(const Node48 &n, vec3 ro, vec3 ridir, vec3 e, float tmin, float tmax,
-                                        float t[4], int l[4]) {
-    const uint32_t w3 = fu(n.a.w);
-    // the plane scales from their exponent bytes: bit-identical to the 64-B node's floats
-    const float sx = __uint_as_float((w3 << 23) & 0x7F800000u);
-    const float sy = __uint_as_float((w3 << 15) & 0x7F800000u);
-    const float sz = __uint_as_float((w3 << 7) & 0x7F800000u);
-    visit_q(n.a.x, n.a.y, n.a.z, sx, sy, sz, fu(n.b.x), fu(n.b.y), fu(n.b.z), fu(n.b.w), fu(n.c.x), fu(n.c.y), ro,
-            ridir, e, tmin, tmax, t);
-    // child k: ~(((base + offset_k) << 3) | code_k) = ~(base << 3) - byte_k
-    const uint32_t nb3 = ~(fu(n.c.z) << 3), bytes = fu(n.c.w);
-#pragma unroll
-    for (int k = 0; k < 4; k++) l[k] = (int)(nb3 - ((bytes >> (8 * k)) & 0xFFu));
-    sort4(t, l);
-}
-
 
 // Node fetch by a 32-bit byte offset from the uniform base (the engine keeps node
 // arrays to at most 2^26 nodes = 4 GiB, kMaxNodes4), which the compiler turns into

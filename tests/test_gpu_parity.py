@@ -409,36 +409,6 @@ def test_one_launch_frames_match_oracle(case, monkeypatch):
         (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
 
 
-@pytest.mark.parametrize("case", ["flat", "flat_64b", "materials_world", "materials_object"])
-def test_node48_layout_matches_oracle(case, monkeypatch):
-    """The 48-B traversal layout (csrc/bvh48.hip: nodes and leaf records in one slot array, a
-    node's children one contiguous block) runs for flat and world-mode scenes, the 64-B kernels
-    for object-mode two-level scenes and under PUPIL_NODE48=0; every pixel, AOV and ray count
-    equals the oracle's either way (stats, multi-material bins and the shading records indexed
-    by 48-B slot included)."""
-    if case == "flat_64b":
-        monkeypatch.setenv("PUPIL_NODE48", "0")
-    if case.startswith("materials"):
-        monkeypatch.setenv("PUPIL_ACCEL", "two_level")
-        monkeypatch.setenv("PUPIL_TL_MODE", "world" if case.endswith("world") else "object")
-        desc = World().load_scene(scenes.cornell_materials_xml(os.path.join(TMP, "cbmat64.xml"), 64, 64, 6)).desc()
-    else:
-        desc = scenes.sphere_field(27, 128, 80, 4, seed=3).desc()
-    gpu = render_gpu(desc, 2, stats=True)
-    s = gpu["stats"]
-    if case in ("flat", "materials_world"):
-        assert s["traversal_slots48"] > s["bvh_nodes"] // 2
-    else:
-        assert s["traversal_slots48"] == 0
-    ref = oracle.OracleScene(desc).render(spp=2)
-    assert compare(gpu, ref, f"node48-{case}") == len(ref["accum"])
-    assert np.array_equal(gpu["albedo"], ref["albedo"]) and np.array_equal(gpu["normal"], ref["normal"])
-    assert np.array_equal(gpu["test"].reshape(-1), ref["test"])
-    rs = ref["stats"]
-    assert (s["primary_rays"], s["extension_rays"], s["shadow_rays"]) == \
-        (rs["primary_rays"], rs["extension_rays"], rs["shadow_rays"])
-
-
 def test_non_accumulating_frame_overwrites():
     desc = _cornell(32).desc()
     a = render_gpu(desc, 1, seed=5, accumulate=False)
