@@ -468,11 +468,13 @@ uint64_t nodes4_count(const pupil_pt *pt) {
 int refresh_node_bound(pupil_pt *pt) {
     pt->sc.node_bound[0] = pt->sc.node_bound[1] = pt->sc.node_bound[2] = 0.f;
     const uint64_t n = nodes4_count(pt);
-    {  // LDS-resident top of the tree (pt_scene.h top_nodes); two-level: within the TLAS
-        static const uint32_t want = [] {
-            const char *e = std::getenv("PUPIL_TOP_NODES");
-            return e ? (uint32_t)std::min<long>(kTopNodes, std::max(0L, std::atol(e))) : kTopNodes;
-        }();
+    {  // LDS-resident top of the tree (pt_scene.h top_nodes) for the world-mode two-level structure, whose
+       // braided TLAS every ray crosses first: -1.3 % per config-5 step; the flat trees of configs 3 / 4
+       // pay 1.1 % per launch for the per-visit branch and run the kernel without it
+       // (profiles/r05_top_nodes_bisect.txt; PUPIL_TOP_NODES=k forces k nodes, 0 off)
+        const char *e = std::getenv("PUPIL_TOP_NODES");
+        const uint32_t want = e ? (uint32_t)std::min<long>(kTopNodes, std::max(0L, std::atol(e)))
+                                : (pt->two_level && pt->tl.world ? kTopNodes : 0u);
         uint64_t live = pt->sc.nodes4 ? n : 0;
         if (pt->two_level) live = std::min<uint64_t>(live, pt->tl.tlas_nodes);
         pt->sc.top_nodes = (uint32_t)std::min<uint64_t>(want, live);

@@ -43,15 +43,17 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
 // instance each; entering one pushes the pending TLAS link and kReturnLink and
 // switches the box tests to the instance's object-space ray; popping
 // kReturnLink switches back.  Spheres are tested at their TLAS leaf.
-template <int MODE, bool ANY, bool STATS, bool TL>
+// TOP: nodes [0, sc.top_nodes) are read from an LDS copy (DeviceScene::top_nodes; a separate
+// instance, since the per-visit LDS-or-global branch costs 1.1 % where the copy does not pay)
+template <int MODE, bool ANY, bool STATS, bool TL, bool TOP = false>
 __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathState &ps, const Queues &q,
                                             const TraceJob &job, int *ovf, uint32_t ovf_threads,
                                             const TraceStats &stats, int *s_ring, float *s_aux, float *s_tst,
                                             Bvh4Node *s_top) {
     constexpr float kInf = __builtin_huge_valf();
     // the top of the tree (nodes [0, top), breadth first) into LDS: every ray starts there
-    const uint32_t top = TL ? 0u : sc.top_nodes;
-    if (!TL) {
+    const uint32_t top = TOP ? sc.top_nodes : 0u;
+    if (TOP) {
         for (uint32_t i = threadIdx.x; i < top * 4u; i += kTraceBlock)
             reinterpret_cast<float4 *>(s_top)[i] = reinterpret_cast<const float4 *>(sc.nodes4)[i];
         __syncthreads();
@@ -230,7 +232,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
         if (active) {
             while ((uint32_t)node < (uint32_t)kSentinel) {
                 Bvh4Node n;
-                if ((uint32_t)node < top) n = s_top[node];
+                if (TOP && (uint32_t)node < top) n = s_top[node];
                 else n = load_node4(sc, node);
                 if (STATS) {
                     if (kMixed && any) nv_sh++;
@@ -424,14 +426,14 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     }
 }
 
-template <int MODE, bool ANY, bool STATS>
+template <int MODE, bool ANY, bool STATS, bool TOP>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4(
     DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
     __shared__ int s_ring[kRing * kTraceBlock];
     __shared__ float s_aux[4 * kTraceBlock];
     __shared__ float s_tst[STATS ? kRing * kTraceBlock : 1];
     __shared__ Bvh4Node s_top[kTopNodes];
-    trace4_body<MODE, ANY, STATS, false>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst, s_top);
+    trace4_body<MODE, ANY, STATS, false, TOP>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst, s_top);
 }
 
 // two-level variant: 9 more live registers (object-space box ray, margin,
@@ -475,12 +477,19 @@ static void launch_trace4(const DeviceScene &sc, const PathState &ps, const Queu
         else
             hipLaunchKernelGGL((k_trace4tl<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
                                ovf, ovf_threads, st);
+    } else if (sc.top_nodes) {
+        if (stats)
+            hipLaunchKernelGGL((k_trace4<MODE, ANY, true, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                               ovf, ovf_threads, st);
+        else
+            hipLaunchKernelGGL((k_trace4<MODE, ANY, false, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                               ovf, ovf_threads, st);
     } else if (stats) {
-        hipLaunchKernelGGL((k_trace4<MODE, ANY, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
-                           ovf_threads, st);
+        hipLaunchKernelGGL((k_trace4<MODE, ANY, true, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                           ovf, ovf_threads, st);
     } else {
-        hipLaunchKernelGGL((k_trace4<MODE, ANY, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job, ovf,
-                           ovf_threads, st);
+        hipLaunchKernelGGL((k_trace4<MODE, ANY, false, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, ps, q, job,
+                           ovf, ovf_threads, st);
     }
 }
 

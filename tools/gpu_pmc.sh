@@ -16,7 +16,7 @@ for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INS
   [ "$rc" -eq 0 ] || exit $rc
 done
 cd $R
-K=${PMC_KERNELS:-"k_trace4<0, false, false>|k_trace4<3, false, false>|k_trace4<4, false, false>"}
+K=${PMC_KERNELS:-"k_trace4<0, false, false, false>|k_trace4<3, false, false, false>|k_trace4<4, false, false, false>|k_trace4<0, false, false, true>|k_trace4<3, false, false, true>|k_trace4<4, false, false, true>"}
 PUPIL_ROUND=${PUPIL_ROUND:-r05} python3 tools/pmc_summary.py gpurun_out/pmc --json "$K" gpurun_out/pmc_config$CFG.json \
   "config $CFG default bench: all non-instrumented k_trace4 launches (primary extend, mixed extension/shadow, pipelined mixed + camera rays)"
 python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt

@@ -65,7 +65,7 @@ for step in ${STEPS:-suite smoke}; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 4 --cpu-baseline 0 --dropin 0 ${BENCH4_ARGS:-} > $O/prof.log 2>&1
     rc=$?; cd $R; [ $rc -eq 0 ] || { tail -5 $O/prof.log; exit $rc; }
     python3 tools/kstats.py $O/prof/run_kernel_stats.csv > $O/kernel_stats.txt
-    python3 tools/timed_kernels.py $O/prof/run_kernel_trace.csv "k_trace4<4, false, false>" 5 > $O/timed_kernels.txt
+    python3 tools/timed_kernels.py $O/prof/run_kernel_trace.csv "${PROF_KERNEL:-k_trace4<4, false, false, false>}" 5 > $O/timed_kernels.txt
     grep '^{' $O/prof.log | tail -1 > $O/prof_bench.json
     tail -1 $O/timed_kernels.txt; rm -f $O/prof/*.csv.gz ;;
   ranks)

@@ -2,7 +2,7 @@
 the basic blocks between two markers (default: the BVH4 node loop of k_trace4, from
 the block holding the node's four global_load_dwordx4 up to the stack pushes).
 
-usage: python tools/isa_loop.py build/obj/pt_kernels.o "k_trace4<4, false, false>" [out.s]
+usage: python tools/isa_loop.py build/obj/pt_kernels.o "k_trace4<4, false, false, false>" [out.s]
 Prints per-class counts (VALU, SALU, VMEM, LDS) of the whole kernel and of the node
 loop body (the straight-line path from the node fetch to the next fetch's branch)."""
 import os

@@ -2,7 +2,7 @@
 and the mean of the last N (the timed region of a bench run, whose traversal launches
 are the last ones of their kernel).
 
-usage: python tools/timed_kernels.py run_kernel_trace.csv "k_trace4<4, false, false>" [N]
+usage: python tools/timed_kernels.py run_kernel_trace.csv "k_trace4<4, false, false, false>" [N]
 """
 import csv
 import re
