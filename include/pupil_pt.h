@@ -305,6 +305,12 @@ typedef struct pupil_pt_counters {
     /* renders run as one persistent launch per frame (renders that start no frame ahead and
      * have at most PUPIL_FRAME_PATHS paths: the moving-camera OnRun, one rank's tiles) */
     uint64_t frame_launches;
+    /* ABI 6.  Device time of those one-launch frames (collect_stats bit 1 / 2): the frame kernel
+     * traces and shades, so it is kept out of trace_ms; PUPIL_COOP builds (collect_stats bit 0):
+     * the cooperative node fetch's LDS-DMA wave-instructions and node slots */
+    double frame_ms;
+    uint64_t coop_dma;
+    uint64_t coop_slots;
 } pupil_pt_counters;
 
 typedef struct pupil_pt pupil_pt;

@@ -97,7 +97,9 @@ class Counters(C.Structure):
                 # ABI 5
                 ("node_loop_iters", C.c_uint64), ("node_loop_lanes", C.c_uint64), ("leaf_loop_iters", C.c_uint64),
                 ("leaf_loop_lanes", C.c_uint64), ("refills", C.c_uint64), ("refill_lanes", C.c_uint64),
-                ("frame_launches", C.c_uint64)]
+                ("frame_launches", C.c_uint64),
+                # ABI 6
+                ("frame_ms", C.c_double), ("coop_dma", C.c_uint64), ("coop_slots", C.c_uint64)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_ if name != "pad_counters"}

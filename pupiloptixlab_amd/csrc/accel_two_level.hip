@@ -838,10 +838,21 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     }
     // world-mode leaf links name world record slots (the meshes' copies, then one 2-slot leaf
     // per sphere) in 28 bits: beyond that the object-space structure serves the scene
-    if (acc.world && two_level_fit(slots64, wbase, spheres, n, true) != TwoLevelFit::World) {
+    // PUPIL_DEBUG_TL_FALLBACK (tests only): force the fallback below (1) or the node-limit one (2)
+    const int force_fallback = [] {
+        const char *e = std::getenv("PUPIL_DEBUG_TL_FALLBACK");
+        return e ? std::atoi(e) : 0;
+    }();
+    // object mode keeps only the per-instance TLAS slots [0, max(1, n)) before its BLASes
+    // (node_base): the braided reserve sized above must go with world mode
+    auto to_object_mode = [&]() {
+        acc.world = false;
+        acc.tlas_cap = std::max(1u, n);
+    };
+    if (acc.world && (force_fallback == 1 || two_level_fit(slots64, wbase, spheres, n, true) != TwoLevelFit::World)) {
         std::fprintf(stderr, "[pupil] two-level: %llu world record slots + %llu spheres exceed the 28-bit leaf links, object mode\n",
                      (unsigned long long)wbase, (unsigned long long)spheres);
-        acc.world = false;
+        to_object_mode();
     }
     int trc = 0;
     if (wbase >= (1ull << 31) ||
@@ -854,10 +865,10 @@ int build_two_level(const std::vector<TwoLevelShape> &shapes, const std::vector<
     acc.num_wprims = (uint32_t)wbase;
     // the traversal addresses nodes by 32-bit offsets (kMaxNodes4): instance copies beyond
     // that take the object-space structure, whose BLASes are shared
-    if (acc.world && wnodes > kMaxNodes4) {
+    if (acc.world && (force_fallback == 2 || wnodes > kMaxNodes4)) {
         std::fprintf(stderr, "[pupil] two-level: %llu world BLAS copy nodes exceed the node limit, object mode\n",
                      (unsigned long long)wnodes);
-        acc.world = false;
+        to_object_mode();
     }
     if (acc.world) {  // world BLAS copies + sphere records appended to the world records
         acc.entries.assign(n, {});

@@ -176,7 +176,7 @@ struct pupil_pt {
     uint64_t last_primary = 0;
     bool last_stats = false;
     std::vector<hipEvent_t> trace_events;  // pairs
-    std::vector<uint8_t> pair_kind;        // per pair: 0 extend, 1 shadow, 2 shade
+    std::vector<uint8_t> pair_kind;        // per pair: 0 extend, 1 shadow / mixed traversal, 2 shade, 3 one-launch frame
     // ev_begin / ev_end bracket renders that collect counters or stage times only (each event
     // leaves a few us of stream gap); ev_sync orders another stream after the last render
     hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_sync = nullptr;
@@ -184,8 +184,8 @@ struct pupil_pt {
     uint32_t trace_pairs = 0;
     bool pairs_keep = false;  // the pairs of PUPIL_STATS_TRACE_TIMING renders accumulate until read
     // pairs of a PUPIL_STATS_TRACE_TIMING sequence folded into sums once kMaxPairs are pending
-    double kept_ms[3] = {0.0, 0.0, 0.0};
-    uint64_t kept_n[3] = {0, 0, 0};
+    double kept_ms[4] = {0.0, 0.0, 0.0, 0.0};
+    uint64_t kept_n[4] = {0, 0, 0, 0};
     uint64_t refits = 0;  // acceleration structure refits / rebuilds after instance updates
     // PUPIL_TRACE_TAIL: per-wave start / drained / exit times of each traversal launch of a stats render
     unsigned long long *tail_buf = nullptr;
@@ -699,7 +699,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         pt->snap_taken = true;
         FrameParams fs = fp;
         fs.group = 1;
-        cx.ev0(1);
+        cx.ev0(3);  // traversal and shading in one kernel: timed apart from trace_ms (frame_ms)
         launch_frame(pt->sc, fs, ring, pt->q.work + kWorkFrame, pt->ray_cum, pt->ovf, pt->ovf_threads,
                      interleave0 && fp.spp > 1 ? fp.spp : 0u, s);
         cx.ev1();
@@ -820,7 +820,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
 extern "C" {
 
 const char *pupil_last_error(void) { return g_last_error.c_str(); }
-int pupil_abi_version(void) { return 5; }
+int pupil_abi_version(void) { return 6; }
 
 int pupil_pt_local_pixels(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t tile_rank, uint32_t tile_world,
                           uint32_t *out_pixels, uint32_t *inout_count) {
@@ -1064,7 +1064,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     std::memcpy(sc.camera.c2w, scene->camera_to_world, sizeof(sc.camera.c2w));
     // traversal overflow stacks, counters, events
     pt->ovf_threads = trace_grid_blocks() * (uint32_t)kTraceBlock;
-    if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * kStackOvf) || pt->alloc(&pt->trace_counters, 32) ||
+    if (pt->alloc(&pt->ovf, (size_t)pt->ovf_threads * std::max(kStackOvf, kTraceStackOvf)) || pt->alloc(&pt->trace_counters, 32) ||
         pt->alloc(&pt->ray_cum, 4) || pt->alloc(&pt->node_bound, 3) || pt->alloc(&pt->q.counts, kCountSlots) ||
         pt->alloc(&pt->q.work, kWorkSlots))
         return cleanup(fail(PUPIL_ERR_OOM, "workspace allocation failed"));
@@ -1298,7 +1298,7 @@ int pupil_pt_render(pupil_pt *pt, const pupil_pt_frame *out, const pupil_pt_laun
     cx.trace_only = trace_timing;
     if (!(trace_timing && pt->pairs_keep)) {  // a new sum
         pt->trace_pairs = 0;
-        for (int k = 0; k < 3; k++) pt->kept_ms[k] = 0.0, pt->kept_n[k] = 0;
+        for (int k = 0; k < 4; k++) pt->kept_ms[k] = 0.0, pt->kept_n[k] = 0;
     }
     if (trace_timing && pt->trace_pairs >= kMaxPairs) {  // a long unread sequence: fold the pending pairs
         HIP_TRY(hipEventSynchronize(pt->trace_events[2 * pt->trace_pairs - 1]));
@@ -1374,8 +1374,8 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
         float ms = 0.f;
         if (pt->last_timed) HIP_TRY(hipEventElapsedTime(&ms, pt->ev_begin, pt->ev_end));
         c.last_render_ms = ms;
-        double kind_ms[3] = {pt->kept_ms[0], pt->kept_ms[1], pt->kept_ms[2]};
-        uint64_t kind_n[3] = {pt->kept_n[0], pt->kept_n[1], pt->kept_n[2]};
+        double kind_ms[4] = {pt->kept_ms[0], pt->kept_ms[1], pt->kept_ms[2], pt->kept_ms[3]};
+        uint64_t kind_n[4] = {pt->kept_n[0], pt->kept_n[1], pt->kept_n[2], pt->kept_n[3]};
         for (uint32_t i = 0; i < pt->trace_pairs; i++) {
             float m = 0.f;
             HIP_TRY(hipEventElapsedTime(&m, pt->trace_events[2 * i], pt->trace_events[2 * i + 1]));
@@ -1388,6 +1388,7 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
         c.extend_ms = kind_ms[0];
         c.extend_launches = kind_n[0];
         c.shade_ms = kind_ms[2];
+        c.frame_ms = kind_ms[3];
         if (pt->last_stats && pt->tail_buf && pt->tail_launches) {  // PUPIL_TRACE_TAIL summary on stderr
             std::vector<unsigned long long> tb((size_t)pt->tail_launches * pt->tail_waves * 4);
             HIP_TRY(hipMemcpy(tb.data(), pt->tail_buf, sizeof(unsigned long long) * tb.size(), hipMemcpyDeviceToHost));
@@ -1430,6 +1431,12 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
                              100.0 * (double)d[3] / (64.0 * (double)std::max(1ull, d[2])), d[4],
                              (double)d[5] / (double)std::max(1ull, d[4]), visits, 100.0 * (double)tc[9] / visits,
                              100.0 * (double)tc[8] / visits);
+                if (tc[24])  // PUPIL_COOP builds: the cooperative node fetch
+                    std::fprintf(stderr,
+                                 "[pupil] coop fetch: %llu LDS-DMA wave-instructions (%.2f per node-loop iteration), "
+                                 "%llu node slots (%.1f%% of the node visits, %.1f per DMA)\n",
+                                 tc[24], (double)tc[24] / (double)std::max(1ull, d[0]), tc[25],
+                                 100.0 * (double)tc[25] / visits, (double)tc[25] / (double)tc[24]);
             }
             c.node_loop_iters = tc[2];  // trace4_body dg[0..5]
             c.node_loop_lanes = tc[3];
@@ -1441,6 +1448,8 @@ int pupil_pt_stats(pupil_pt *pt, pupil_pt_counters *out) {
             c.prim_tests = tc[1] + tc[15];
             c.shadow_rays_reference = tc[16];
             c.unique_node_fetches = tc[18];
+            c.coop_dma = tc[24];
+            c.coop_slots = tc[25];
             c.queue_handed = tc[20];
             c.queue_activated = tc[21];
             c.queue_retired = tc[22];
@@ -1513,7 +1522,7 @@ int pupil_pt_trace_rays(pupil_pt *pt, uint32_t n, const float *rays, float *out,
         pt->last_timed = true;
         pt->snap_taken = false;
         pt->trace_pairs = 0;
-        for (int k = 0; k < 3; k++) pt->kept_ms[k] = 0.0, pt->kept_n[k] = 0;
+        for (int k = 0; k < 4; k++) pt->kept_ms[k] = 0.0, pt->kept_n[k] = 0;
         pt->rendered = true;
         pt->last_stream = pt->own_stream;
     }

@@ -17,11 +17,32 @@ constexpr int kTraceWavesPerSimd = 7;
 constexpr int kTraceWavesPerSimdTL = 5;  // two-level variant (<= 96 VGPRs; A/B r02 on config 5: 4 waves 688, 5: 743, 6: 716 Mrays/s)
 constexpr int kStackOvf = 160;  // per-thread global overflow entries
 constexpr int kRing = 16;       // persistent BVH4 kernels: per-lane LDS ring entries (spills to the overflow column)
+// Wave-cooperative node fetch in k_trace4 (pt_traverse.h CoopFetch): 0 = each lane loads its own
+// node (four 16-B loads per visit), 1 = the wave's distinct nodes are loaded a quarter per lane
+// into a per-wave LDS image and read back from there
+#ifndef PUPIL_COOP
+#define PUPIL_COOP 0
+#endif
+constexpr bool kCoopFetch = PUPIL_COOP != 0;
+// nodes one round of the cooperative fetch stages (16 per LDS-DMA wave-instruction)
+#ifndef PUPIL_COOP_CHUNKS
+#define PUPIL_COOP_CHUNKS 1
+#endif
+constexpr int kCoopChunks = PUPIL_COOP_CHUNKS;
+// k_trace4's LDS ring: the cooperative fetch's staging (1 KiB + 256 B per wave and chunk) comes
+// out of the ring so 14 blocks still fit a CU's 160 KiB
+#ifndef PUPIL_TRACE_RING
+#define PUPIL_TRACE_RING (PUPIL_COOP ? 13 : 16)
+#endif
+constexpr int kTraceRing = PUPIL_TRACE_RING;
+static_assert(kTraceRing >= 8 && kTraceRing <= kRing, "trace ring");
 // Stack entries a traversal may need: 3 per BVH4 level (4 children, one taken), plus
 // 2 per instance entry in two-level mode.  Builds whose trees need more are rejected
 // (or rebuilt with the depth-bounded Karras LBVH) at create time, so no kernel ever
 // overwrites a live entry.
 constexpr int kTraceStackEntries = kRing + kStackOvf;
+// a smaller trace ring spills into a deeper overflow column: capacity >= kTraceStackEntries
+constexpr int kTraceStackOvf = kStackOvf + (kRing - kTraceRing + 7) / 8 * 8;
 constexpr int kShadeBlock = 256;
 constexpr uint32_t kMaxDepth = 128;  // PTPass inspector range (pt_pass.cpp:225-237)
 constexpr uint32_t kNumQueues = 9;  // 0 = miss, 1..7 = EMatType, 8 = unknown material

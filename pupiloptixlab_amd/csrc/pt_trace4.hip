@@ -45,11 +45,14 @@ __device__ __forceinline__ void enter_instance(const DevInstance &in, const RayP
 // kReturnLink switches back.  Spheres are tested at their TLAS leaf.
 // TOP: nodes [0, sc.top_nodes) are read from an LDS copy (DeviceScene::top_nodes; a separate
 // instance, since the per-visit LDS-or-global branch costs 1.1 % where the copy does not pay)
-template <int MODE, bool ANY, bool STATS, bool TL, bool TOP = false>
+// COOP: the wave-cooperative node fetch (pt_traverse.h CoopFetch; flat kernels only), staged in
+// s_coop (per wave: 64 node offsets, then the 16 * kCoopChunks node image); the stack ring is
+// RING entries (kTraceRing when COOP, leaving the LDS for the staging)
+template <int MODE, bool ANY, bool STATS, bool TL, bool TOP = false, bool COOP = false, int RING = kRing>
 __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathState &ps, const Queues &q,
                                             const TraceJob &job, int *ovf, uint32_t ovf_threads,
                                             const TraceStats &stats, int *s_ring, float *s_aux, float *s_tst,
-                                            Bvh4Node *s_top) {
+                                            Bvh4Node *s_top, float4 *s_coop = nullptr) {
     constexpr float kInf = __builtin_huge_valf();
     // the top of the tree (nodes [0, top), breadth first) into LDS: every ray starts there
     const uint32_t top = TOP ? sc.top_nodes : 0u;
@@ -63,13 +66,21 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     // mixed launches may carry the next render's camera rays (render-ahead, TraceJob::ahead_off)
     const uint32_t n_ahead = MODE == kModeMixedAhead ? job.static_count : 0u;
     const uint32_t count = kMixed ? n_next + q.counts[kCntShadow] : (job.count_ptr ? *job.count_ptr : job.static_count);
-    LinStack st;
+    LinStackT<RING, COOP ? kTraceStackOvf : kStackOvf> st;
     st.lds = s_ring + threadIdx.x;
     st.ovf_blk = ovf + blockIdx.x * blockDim.x;
     st.lds0 = s_ring;
     st.ovf_stride = ovf_threads;
     if (STATS) st.tcol = s_tst + threadIdx.x;
     st.reset();
+    CoopFetch<kCoopChunks> cf;
+    if (COOP) {
+        // this wave's staging: 256 B of node offsets, then the node image (wave-uniform base)
+        const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        float4 *wbase = s_coop + w * (16u + 64u * kCoopChunks);
+        cf.addr = reinterpret_cast<uint32_t *>(wbase);
+        cf.stage = wbase + 16;
+    }
     // STATS: visits of a popped node whose entry distance already exceeds the ray's tmax (a
     // stack holding distances could skip them without the fetch), visits where no child was hit
     uint32_t n_cullable = 0, n_nohit = 0;
@@ -229,54 +240,72 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             continue;
         }
         // ---- traverse until this lane's ray terminates or it needs a leaf while others do too
-        if (active) {
-            while ((uint32_t)node < (uint32_t)kSentinel) {
-                Bvh4Node n;
-                if (TOP && (uint32_t)node < top) n = s_top[node];
-                else n = load_node4(sc, node);
-                if (STATS) {
-                    if (kMixed && any) nv_sh++;
-                    else nv++;
-                    const unsigned long long m = __ballot(true);
-                    if ((int)lane_id() == __ffsll((long long)m) - 1) {
-                        dg[0]++;
-                        dg[1] += (unsigned long long)__popcll(m);
-                    }
-                    // distinct nodes fetched by this wave step (lanes of a wave on the same node
-                    // share one fetch): the gather rate the memory system actually serves
-                    bool dup = false;
-                    for (int j = 0; j < 64; j++) {
-                        const int nj = __shfl(node, j);
-                        if (j < (int)lane_id() && ((m >> j) & 1ull) && nj == node) dup = true;
-                    }
-                    n_unique += dup ? 0u : 1u;
-                }
-                float t[4];
-                int l[4];
-                if (TL) visit4(n, bo, bi, be, tmin, tmax, t, l);
-                else visit4(n, r.o, r.idir, be, tmin, tmax, t, l);
-                if (STATS) {
-                    n_cullable += t_node > tmax ? 1u : 0u;
-                    n_nohit += t[0] == kInf ? 1u : 0u;
-                }
-                if (t[0] == kInf) {
-                    node = st.pop();
-                    if (STATS) t_node = st.tpop;
-                } else {
-                    node = l[0];
-                    if (STATS) t_node = t[0];
-                    st.reserve3();
-                    st.push3t(t[1], t[2], t[3], t[2] != kInf, t[3] != kInf);
-                    st.push3(l[1], l[2], l[3], t[1] != kInf, t[2] != kInf, t[3] != kInf);
-                    if (node == kEmptyLink) node = st.pop();  // degenerate child boxes only (LinStack)
-                }
-                if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
-                    leaf = node;
-                    node = st.pop();
-                    if (STATS) t_node = st.tpop;
-                }
+        // one node visit of this lane (node phase): box test, push / pop, postpone a leaf
+        auto visit_node = [&](const Bvh4Node &n) {
+        if (STATS) {
+            if (kMixed && any) nv_sh++;
+            else nv++;
+            const unsigned long long m = __ballot(true);
+            if ((int)lane_id() == __ffsll((long long)m) - 1) {
+                dg[0]++;
+                dg[1] += (unsigned long long)__popcll(m);
+            }
+            // distinct nodes fetched by this wave step (lanes of a wave on the same node
+            // share one fetch): the gather rate the memory system actually serves
+            bool dup = false;
+            for (int j = 0; j < 64; j++) {
+                const int nj = __shfl(node, j);
+                if (j < (int)lane_id() && ((m >> j) & 1ull) && nj == node) dup = true;
+            }
+            n_unique += dup ? 0u : 1u;
+        }
+        float t[4];
+        int l[4];
+        if (TL) visit4(n, bo, bi, be, tmin, tmax, t, l);
+        else visit4(n, r.o, r.idir, be, tmin, tmax, t, l);
+        if (STATS) {
+            n_cullable += t_node > tmax ? 1u : 0u;
+            n_nohit += t[0] == kInf ? 1u : 0u;
+        }
+        if (t[0] == kInf) {
+            node = st.pop();
+            if (STATS) t_node = st.tpop;
+        } else {
+            node = l[0];
+            if (STATS) t_node = t[0];
+            st.reserve3();
+            st.push3t(t[1], t[2], t[3], t[2] != kInf, t[3] != kInf);
+            st.push3(l[1], l[2], l[3], t[1] != kInf, t[2] != kInf, t[3] != kInf);
+            if (node == kEmptyLink) node = st.pop();  // degenerate child boxes only (LinStack)
+        }
+        if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
+            leaf = node;
+            node = st.pop();
+            if (STATS) t_node = st.tpop;
+        }
+        };
+        if (COOP) {
+            // wave-uniform node phase: every lane takes part in the fetch, lanes that need a
+            // node visit it (the same visits in the same order per lane as the loop below)
+            for (;;) {
+                const bool want = active && (uint32_t)node < (uint32_t)kSentinel;
+                if (!__any(want)) break;
+                const Bvh4Node n = cf.template fetch<STATS>(sc.nodes4, node, want);
+                if (want) visit_node(n);
                 // leave for the leaf phase once fewer than node_min lanes still need a node
-                if ((uint32_t)__popcll(__ballot(leaf >= 0)) < job.node_min) break;
+                if ((uint32_t)__popcll(__ballot(want && leaf >= 0)) < job.node_min) break;
+            }
+        }
+        if (active) {
+            if (!COOP) {
+                while ((uint32_t)node < (uint32_t)kSentinel) {
+                    Bvh4Node n;
+                    if (TOP && (uint32_t)node < top) n = s_top[node];
+                    else n = load_node4(sc, node);
+                    visit_node(n);
+                    // leave for the leaf phase once fewer than node_min lanes still need a node
+                    if ((uint32_t)__popcll(__ballot(leaf >= 0)) < job.node_min) break;
+                }
             }
             while (leaf < 0) {
                 if (STATS) {
@@ -387,6 +416,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     flush_stats<STATS>(&stats, nv, npt, 0);
     if (kMixed) flush_stats<STATS>(&stats, nv_sh, npt_sh, 14);
     flush_stats<STATS>(&stats, n_unique, 0u, 18);
+    if (COOP) flush_stats<STATS>(&stats, cf.n_dma, cf.n_slots, 24);
     flush_stats<STATS>(&stats, n_cullable, n_nohit, 8);
     if (STATS && stats.wave_times && lane_id() == 0) {
         unsigned long long *w = stats.wave_times + 4ull * (blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u);
@@ -429,11 +459,15 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
 template <int MODE, bool ANY, bool STATS, bool TOP>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4(
     DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
-    __shared__ int s_ring[kRing * kTraceBlock];
+    constexpr int ring = kCoopFetch ? kTraceRing : kRing;
+    __shared__ int s_ring[ring * kTraceBlock];
     __shared__ float s_aux[4 * kTraceBlock];
-    __shared__ float s_tst[STATS ? kRing * kTraceBlock : 1];
-    __shared__ Bvh4Node s_top[kTopNodes];
-    trace4_body<MODE, ANY, STATS, false, TOP>(sc, ps, q, job, ovf, ovf_threads, stats, s_ring, s_aux, s_tst, s_top);
+    __shared__ float s_tst[STATS ? ring * kTraceBlock : 1];
+    __shared__ Bvh4Node s_top[kCoopFetch ? 1 : kTopNodes];
+    __shared__ float4 s_coop[kCoopFetch ? (kTraceBlock / 64) * (16 + 64 * kCoopChunks) : 1];
+    // the cooperative fetch replaces the LDS top-of-tree copy (its hot nodes are one shared DMA)
+    trace4_body<MODE, ANY, STATS, false, TOP && !kCoopFetch, kCoopFetch, ring>(sc, ps, q, job, ovf, ovf_threads, stats,
+                                                                              s_ring, s_aux, s_tst, s_top, s_coop);
 }
 
 // two-level variant: 9 more live registers (object-space box ray, margin,

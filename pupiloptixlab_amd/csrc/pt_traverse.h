@@ -140,7 +140,8 @@ constexpr int kSpill = 8;
 // a full column spills its bottom 8 entries and moves the top ones down (rare: deep trees).
 // Popping an empty child slot (kEmptyLink, possible only for degenerate child boxes whose
 // empty planes the conservative slab bound lets through) pops again.
-struct LinStack {
+template <int RING, int OVF, int SPILL = (RING >= 11 ? kSpill : RING / 2)>
+struct LinStackT {
     int *lds;  // this lane's column (stride kTraceBlock)
     int *ovf_blk;
     const int *lds0;
@@ -151,7 +152,7 @@ struct LinStack {
     }
     uint32_t ovf_stride;
     int sp;   // entries in the LDS column
-    int nsp;  // entries in the overflow column (multiple of kSpill)
+    int nsp;  // entries in the overflow column (multiple of SPILL)
     // counter kernels only (null otherwise, compiled out): the entry distance of every LDS
     // entry in a parallel column, so a pop can tell whether the node lies beyond the ray's
     // current tmax (PUPIL_TRACE_DIAG "cullable visits"); entries reloaded from the overflow
@@ -162,18 +163,18 @@ struct LinStack {
     __device__ __forceinline__ int &slot(int i) { return lds[i * kTraceBlock]; }
     __device__ __forceinline__ void reset() { sp = nsp = 0; }
     __device__ __forceinline__ void reserve3() {
-        if (sp > kRing - 3 && nsp + kSpill <= kStackOvf) {
+        if (sp > RING - 3 && nsp + SPILL <= OVF) {
             int *ovf = ovf_col();
 #pragma unroll
-            for (int k = 0; k < kSpill; k++) ovf[(uint32_t)(nsp + k) * ovf_stride] = slot(k);
+            for (int k = 0; k < SPILL; k++) ovf[(uint32_t)(nsp + k) * ovf_stride] = slot(k);
 #pragma unroll
-            for (int k = kSpill; k < kRing; k++)
+            for (int k = SPILL; k < RING; k++)
                 if (k < sp) {
-                    slot(k - kSpill) = slot(k);
-                    if (tcol) tcol[(k - kSpill) * kTraceBlock] = tcol[k * kTraceBlock];
+                    slot(k - SPILL) = slot(k);
+                    if (tcol) tcol[(k - SPILL) * kTraceBlock] = tcol[k * kTraceBlock];
                 }
-            nsp += kSpill;
-            sp -= kSpill;
+            nsp += SPILL;
+            sp -= SPILL;
         }
     }
     __device__ __forceinline__ void push(int v) {
@@ -196,14 +197,14 @@ struct LinStack {
     __device__ __forceinline__ int pop_raw() {
         if (sp == 0) {
             if (nsp == 0) return kSentinel;
-            nsp -= kSpill;
+            nsp -= SPILL;
             const int *ovf = ovf_col();
 #pragma unroll
-            for (int k = 0; k < kSpill; k++) {
+            for (int k = 0; k < SPILL; k++) {
                 slot(k) = ovf[(uint32_t)(nsp + k) * ovf_stride];
                 if (tcol) tcol[k * kTraceBlock] = 0.f;
             }
-            sp = kSpill;
+            sp = SPILL;
         }
         --sp;
         if (tcol) tpop = tcol[sp * kTraceBlock];
@@ -215,6 +216,7 @@ struct LinStack {
         return v;
     }
 };
+using LinStack = LinStackT<kRing, kStackOvf>;
 
 // Child order of a BVH4 visit: the nearest child is descended, the others pushed far to
 // near (r03: partial sorts with 4 or 3 comparators were no faster).  Only the traversal
@@ -328,6 +330,79 @@ __device__ __forceinline__ void visit4(const Bvh4Node &n, vec3 ro, vec3 ridir, v
 __device__ __forceinline__ Bvh4Node load_node4(const DeviceScene &sc, int node) {
     return *reinterpret_cast<const Bvh4Node *>(reinterpret_cast<const char *>(sc.nodes4) + ((uint32_t)node << 6));
 }
+
+// ------------------------------------------------------------------ wave-cooperative node fetch (r06)
+// The per-lane fetch above issues four 16-B loads per visit, and the CU's texture path charges
+// each wave-instruction for all 64 lane slots (~16 cycles) plus every distinct 128-B line its
+// lanes touch (~22 per load at config 4, the same lines four times per visit).
+// Here the wave fetches each distinct node once, a quarter per lane: lanes 4k..4k+3 load node
+// k's four 16-B quarters with one LDS-DMA wave-instruction (16 nodes, 1 KiB, each line touched
+// once), and every lane then reads its node's 64 B from the wave's LDS image (4 ds_read_b128).
+// Distinct nodes: a lane whose lower neighbour wants the same node shares its slot (adjacent
+// lanes hold consecutive work-list items, which agree near the root); that is exact for runs of
+// equal nodes, so slot = leaders below the lane, minus one for a follower.
+// The LDS image is swizzled so the 16 lanes of a ds_read_b128 group meet 16 distinct bank
+// quads: quarter c of slot k sits at 16-B position 4k + ((c + (k >> 2)) & 3); the DMA writes
+// lane-linearly, so lane 4k + q loads quarter (q - (k >> 2)) & 3 (the swizzle goes on the
+// source address, MI355X_MICROARCH.md LDS / cdna_hip_programming.md rule 21).
+__device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+template <int CHUNKS>
+struct CoopFetch {
+    uint32_t *addr;  // this wave's 64 node byte offsets (LDS)
+    float4 *stage;   // this wave's 16 * CHUNKS node image (LDS)
+    // STATS: LDS-DMA wave-instructions issued, node slots fetched
+    uint32_t n_dma = 0, n_slots = 0;
+
+    // Every lane of the wave calls this (full EXEC); lanes with `want` get node `node`.
+    template <bool STATS>
+    __device__ __forceinline__ Bvh4Node fetch(const Bvh4Node *nodes, int node, bool want) {
+        const uint32_t lane = lane_id();
+        // the lower neighbour's wanted node (wave_shr:1; lane 0 sees -1, which no node equals)
+        const int key = want ? node : -1;
+        const int below = __builtin_amdgcn_update_dpp(-1, key, 0x138, 0xF, 0xF, false);
+        const bool lead = want && below != node;
+        const unsigned long long ml = __ballot(lead);
+        const uint32_t n = (uint32_t)__popcll(ml);
+        const uint32_t slot = mbcnt64(ml) - (lead ? 0u : 1u);
+        if (lead) addr[slot] = (uint32_t)node << 6;
+        if (STATS && lane == 0) n_slots += n;
+        const char *base = reinterpret_cast<const char *>(nodes);
+        const uint32_t k = lane >> 2;
+        const uint32_t src_q = ((lane & 3u) - (k >> 2)) & 3u;
+        Bvh4Node out;
+        float4 *o4 = reinterpret_cast<float4 *>(&out);
+        for (uint32_t b = 0; b < n; b += 16u * CHUNKS) {
+#pragma unroll
+            for (int c = 0; c < CHUNKS; c++) {
+                const uint32_t s = b + 16u * c + k;
+                if (s < n) {
+                    const uint32_t off = addr[s] + (src_q << 4);
+                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(base + off),
+                                                     (__attribute__((address_space(3))) void *)(stage + 64 * c), 16, 0,
+                                                     0);
+                }
+                if (STATS && lane == 0 && b + 16u * c < n) n_dma++;
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA writes have landed
+            asm volatile("" ::: "memory");
+            const uint32_t r = slot - b;
+            if (want && r < 16u * CHUNKS) {
+                const uint32_t sw = (r >> 2) & 3u;
+                const float4 *src = stage + 4u * r;
+#pragma unroll
+                for (uint32_t c = 0; c < 4; c++) o4[c] = src[(c + sw) & 3u];
+            }
+            if (b + 16u * CHUNKS < n) {
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): reads done before the next DMA
+                asm volatile("" ::: "memory");
+            }
+        }
+        return out;
+    }
+};
 
 
 }  // namespace tr

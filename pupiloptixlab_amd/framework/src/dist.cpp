@@ -9,6 +9,7 @@
 
 #include <cerrno>
 
+#include <dirent.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -45,6 +46,25 @@ uint64_t proc_start_ticks(long pid) {
         return 0;
     return v;
 }
+
+// wall-clock start of this process (boot time + its start ticks), 0 when unknown
+int64_t self_start_wall() {
+    FILE *f = std::fopen("/proc/stat", "r");
+    if (!f) return 0;
+    char line[256];
+    long long btime = 0;
+    while (std::fgets(line, sizeof(line), f))
+        if (std::sscanf(line, "btime %lld", &btime) == 1) break;
+    std::fclose(f);
+    const long hz = sysconf(_SC_CLK_TCK);
+    const uint64_t ticks = proc_start_ticks((long)getpid());
+    return btime > 0 && hz > 0 && ticks ? (int64_t)btime + (int64_t)(ticks / (uint64_t)hz) : 0;
+}
+
+// an id file whose writer ran on another host (shared filesystem) cannot be checked for
+// liveness: it is taken only if written no earlier than kRemoteIdSlack seconds before this
+// reader started, so a file a crashed launch left long ago is never read
+constexpr int64_t kRemoteIdSlack = 60;
 
 std::string host_name() {
     char h[256] = {0};
@@ -100,7 +120,8 @@ std::string DistLaunchNonce() noexcept {
     // was started (torchrun, mpirun, a slurm step, or a `timeout` wrapper per rank, whose
     // parent processes differ), and another launch differs in its run id / restart count /
     // job step / port.  A stale file of an earlier launch with the same environment is
-    // rejected by its age (exchange_id).
+    // rejected by its writer's liveness on the same host, and by its age against this
+    // process's start for a writer on another host (ReadIdFile).
     auto env = [](const char *k) {
         const char *v = std::getenv(k);
         return std::string(v && *v ? v : "-");
@@ -155,8 +176,16 @@ int ReadIdFile(const std::string &path, const std::string &nonce, void *id, size
         if (read_str(f, host, 255) && std::fread(&pid, sizeof(pid), 1, f) == 1 &&
             std::fread(&start, sizeof(start), 1, f) == 1 && std::fread(id, size, 1, f) == 1) {
             // a writer on this host must still run (rank 0 waits in ncclCommInitRank until every
-            // rank has joined); on a shared filesystem another host's writer is taken on its nonce
-            r = host != host_name() || (start != 0 && proc_start_ticks((long)pid) == start) ? 1 : -1;
+            // rank has joined); on a shared filesystem another host's file must be no older than
+            // this reader's start less kRemoteIdSlack (a relaunch within that window on another
+            // host with the same environment can still meet the earlier launch's file)
+            if (host == host_name()) {
+                r = start != 0 && proc_start_ticks((long)pid) == start ? 1 : -1;
+            } else {
+                struct stat st;
+                const int64_t t0 = self_start_wall();
+                r = fstat(fileno(f), &st) == 0 && (t0 == 0 || (int64_t)st.st_mtime >= t0 - kRemoteIdSlack) ? 1 : -1;
+            }
         } else {
             r = 0;
         }
@@ -176,7 +205,10 @@ DistInfo DistFromEnv() noexcept {
 
 FrameGather::~FrameGather() noexcept {
     Release();
-    if (m_host && m_info.rank == 0) (void)rmdir(m_dir.c_str());  // empty once every frame was consumed
+    if (m_host && m_info.rank == 0) {  // empty once every frame was consumed
+        (void)std::remove((m_dir + "/ready").c_str());
+        (void)rmdir(m_dir.c_str());
+    }
     if (m_comm) (void)ncclCommDestroy(m_comm);
 }
 
@@ -202,6 +234,29 @@ bool FrameGather::Init(const DistInfo &d, int device, const std::string &id_path
         if (mkdir(m_dir.c_str(), 0700) != 0 && errno != EEXIST) {
             Log("rank %d: cannot create %s", d.rank, m_dir.c_str());
             return false;
+        }
+        // rank 0 empties the directory (tile files a crashed earlier run left) and then
+        // publishes a `ready` marker naming itself; the other ranks write no tiles before that
+        // marker exists with a live writer, so no stale f<r>_<frame> is ever read
+        const std::string ready = m_dir + "/ready";
+        if (d.rank == 0) {
+            if (DIR *dir = opendir(m_dir.c_str())) {
+                while (dirent *e = readdir(dir))
+                    if (std::strcmp(e->d_name, ".") != 0 && std::strcmp(e->d_name, "..") != 0)
+                        (void)std::remove((m_dir + "/" + e->d_name).c_str());
+                closedir(dir);
+            }
+            if (!WriteIdFile(ready, DistLaunchNonce(), &d.world, sizeof(d.world))) return false;
+        } else {
+            int world = 0;
+            const auto t0 = std::chrono::steady_clock::now();
+            while (ReadIdFile(ready, DistLaunchNonce(), &world, sizeof(world)) <= 0) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+                    Log("rank %d: no live rank 0 behind %s", d.rank, ready.c_str());
+                    return false;
+                }
+                std::this_thread::sleep_for(std::chrono::milliseconds(2));
+            }
         }
         Log("rank %d of %d: host-staged tile gather through %s (test transport)", d.rank, d.world, m_dir.c_str());
         return true;

@@ -44,7 +44,7 @@ int main(void) {
   S(pupil_texture) S(pupil_material) S(pupil_shape) S(pupil_instance) S(pupil_emitter)
   S(pupil_scene_desc) S(pupil_pt_frame) S(pupil_pt_launch) S(pupil_pt_counters)
   O(pupil_texture, rgba) O(pupil_material, tex) O(pupil_instance, emitter_offset) O(pupil_emitter, radiance)
-  O(pupil_emitter, scale) O(pupil_scene_desc, shapes) O(pupil_scene_desc, env) O(pupil_pt_counters, trace_launches) O(pupil_pt_counters, node_loop_iters) O(pupil_pt_counters, refill_lanes) O(pupil_pt_counters, frame_launches)
+  O(pupil_emitter, scale) O(pupil_scene_desc, shapes) O(pupil_scene_desc, env) O(pupil_pt_counters, trace_launches) O(pupil_pt_counters, node_loop_iters) O(pupil_pt_counters, refill_lanes) O(pupil_pt_counters, frame_launches) O(pupil_pt_counters, frame_ms) O(pupil_pt_counters, coop_slots)
   O(pupil_pt_launch, collect_stats) O(pupil_pt_launch, hints)
   printf("PUPIL_HINT_CONTINUE %u\n", PUPIL_HINT_CONTINUE);
   return 0;

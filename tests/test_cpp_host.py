@@ -243,6 +243,26 @@ def test_rccl_id_file_of_a_finished_writer_is_stale(tmp_path):
     assert lib.pupil_dist_read_id_file(path.encode(), b"launch-x", buf) == 1 and buf.raw == bytes(range(128))
 
 
+def test_rccl_id_file_from_another_host_is_taken_only_when_recent(tmp_path):
+    """On a shared filesystem (PUPIL_RCCL_ID_FILE) a writer on another host cannot be checked
+    for liveness: its file is used only if written no earlier than 60 s before the reader
+    started, so a file a crashed launch left long ago is not read."""
+    _built()
+    import ctypes as C
+    import struct
+
+    lib = C.CDLL(FW)
+    lib.pupil_dist_read_id_file.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p]
+    path = tmp_path / "pupil_rccl.id"
+    nonce, host, ident = b"launch-r", b"another-host.invalid", bytes(range(128))
+    path.write_bytes(b"PUPILID2" + struct.pack("<I", len(nonce)) + nonce + struct.pack("<I", len(host)) + host +
+                     struct.pack("<qQ", 12345, 678) + ident)
+    buf = C.create_string_buffer(128)
+    assert lib.pupil_dist_read_id_file(str(path).encode(), nonce, buf) == 1 and buf.raw == ident
+    os.utime(path, (1, 1))  # written decades before this reader started: a stale launch's file
+    assert lib.pupil_dist_read_id_file(str(path).encode(), nonce, buf) == -1
+
+
 def test_rccl_id_path_agrees_across_differently_started_ranks():
     """Ranks of one launch compute the same id file whatever process started them: here one
     directly and one under a `timeout` wrapper (another parent process), as

@@ -366,14 +366,15 @@ def test_tile_sharding_matches_full_frame():
 
 
 @pytest.mark.parametrize("case", ["cornell", "cornell_spp3_depth7", "materials", "materials_two_level", "field",
-                                  "field_tiles", "field_stages"])
+                                  "field_tiles", "field_stages", "quad_stack"])
 def test_one_launch_frames_match_oracle(case, monkeypatch):
     """Renders that start no frame ahead and are small (PUPIL_FRAME_PATHS) run as ONE persistent
     launch per frame (pt_frame.hip): per-wave rounds of traversal (a bounce's shadow and
     extension rays together) and shading, no partitions.  Every pixel, AOV and ray count equals
     the oracle's: single-material and all-material shading, the two-level world structure, several
     samples per pixel, depth 7, one rank's compact tiles; "field_stages" (PUPIL_FRAME_PATHS=0) is
-    the same render through the stage pipeline."""
+    the same render through the stage pipeline; "quad_stack" (6,000 stacked quads) takes
+    k_frame's traversal stack past its LDS ring into the HBM overflow column and back."""
     import ctypes as C
 
     if case == "field_stages":
@@ -384,6 +385,9 @@ def test_one_launch_frames_match_oracle(case, monkeypatch):
     if case.startswith("cornell"):
         desc = _cornell(64, depth=7 if "depth7" in case else 4).desc()
         spp = 3 if "spp3" in case else 1
+    elif case == "quad_stack":
+        desc = _quad_stack(6000).desc()
+        spp = 2
     elif case.startswith("materials"):
         desc = World().load_scene(scenes.cornell_materials_xml(os.path.join(TMP, "cbmat80.xml"), 80, 80, 6)).desc()
         spp = 2
@@ -774,6 +778,35 @@ def test_tlas_reserve_contents_do_not_move_the_node_bound(monkeypatch):
         abi.check(pt._lib.pupil_debug_fill_tlas_reserve(pt._pt, junk))
         assert pt.stats()["node_bound"] == b0, junk
     pt.close_engine()
+
+
+@pytest.mark.parametrize("fallback", [1, 2])
+def test_world_to_object_fallback_keeps_the_blas_nodes(monkeypatch, fallback):
+    """A world-mode two-level build that falls back to object mode (1: world record slots
+    beyond the 28-bit leaf links, 2: world BLAS copies beyond the node limit; forced here by
+    PUPIL_DEBUG_TL_FALLBACK) keeps only the per-instance TLAS slots before the BLASes (ADVICE
+    r05: the braided reserve used to stay, so the node bound skipped BLAS nodes and the
+    reserve fill overwrote them).  Junk written into the reserve changes nothing, and the
+    render equals the oracle's."""
+    import torch
+    from pupiloptixlab_amd.pt_pass import PTPass
+
+    monkeypatch.setenv("PUPIL_ACCEL", "two_level")
+    monkeypatch.setenv("PUPIL_TL_MODE", "world")
+    monkeypatch.setenv("PUPIL_DEBUG_TL_FALLBACK", str(fallback))
+    w = scenes.instanced_field(num_instances=6, width=32, height=18, max_depth=4, seed=3, spheres_per_blas=10)
+    desc = w.desc()
+    pt = PTPass(device=0)
+    pt.set_scene(desc)
+    b0 = pt.stats()["node_bound"]
+    abi.check(pt._lib.pupil_debug_fill_tlas_reserve(pt._pt, 1e30))
+    assert pt.stats()["node_bound"] == b0
+    pt.render(2)
+    torch.cuda.synchronize()
+    img = pt.buffers.get("pt accum buffer").cpu().numpy()
+    pt.close_engine()
+    ref = oracle.OracleScene(desc).render(spp=2)["accum"]
+    assert np.array_equal(img.view(np.uint32), ref.reshape(img.shape).view(np.uint32))
 
 
 def test_moving_camera_cadence_starts_no_frames_ahead():
