@@ -263,6 +263,12 @@ def main(argv=None):
     # denominator of the per-ray PMC figures (tools/pmc_summary.py --json)
     rays_plain_process = st["rays_traced_total"] - rays_counter_frame
 
+    # N > 1: what each rank saw, so a scaling run verifies itself (which rank was slow, that the
+    # communicator held N ranks, what the tile gather cost per step on its side stream)
+    per_rank, comm = None, None
+    if world > 1:
+        per_rank, comm = rank_report(elapsed, rays_local, [h.elapsed_ms() for h in handles[-args.steps:]],
+                                     dev if backend == "nccl" else "cpu")
     t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64,
                      device=dev if backend == "nccl" else "cpu")
     if world > 1:
@@ -376,6 +382,8 @@ def main(argv=None):
                        "stage_ms_per_frame": {"primary_extend": round(ext_ms, 3),
                                               "bounce_trace": round(trace_ms - ext_ms, 3),
                                               "shade": round(shade_ms, 3)}},
+            "ranks": per_rank,
+            "comm": comm,
             "dropin_cpp": dropin,
             "instance_update_ms": update,
             "roofline": roof,
@@ -385,6 +393,31 @@ def main(argv=None):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+def rank_report(elapsed_s, rays_local, gather_ms, device):
+    """Every rank's timed-region view, gathered to all ranks (a collective: every rank calls it):
+    per-rank elapsed ms, rays traced and mean tile-gather ms per step (side-stream events;
+    None without gathers), and the communicator as torch.distributed saw it (backend, world
+    size, the RCCL version torch links)."""
+    import torch
+    import torch.distributed as dist
+
+    g = [x for x in gather_ms if x is not None]
+    mine = torch.tensor([elapsed_s * 1e3, float(rays_local), sum(g) / len(g) if g else -1.0], dtype=torch.float64,
+                        device=device)
+    allr = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(allr, mine)
+    per_rank = [{"rank": r, "elapsed_ms": round(v[0], 3), "rays": int(v[1]),
+                 "gather_ms_per_step": round(v[2], 4) if v[2] >= 0 else None}
+                for r, v in enumerate(x.cpu().tolist() for x in allr)]
+    try:
+        rccl = ".".join(str(x) for x in torch.cuda.nccl.version())
+    except Exception as e:  # noqa: BLE001 - reported, not fatal
+        rccl = f"unknown ({type(e).__name__})"
+    comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "rccl_version": rccl,
+            "ranks_reporting": len(per_rank)}
+    return per_rank, comm
+
 
 def dropin_cadence(args, batched_ms, last_accum):
     """The reference's cadence through the C++ drop-in: examples/path_tracer (System +
@@ -532,6 +565,22 @@ def roofline(args, st_bytes, timed):
                                        "over 256 TAs (one per CU) at the GRBM-measured clock",
                                 "frac_at_spec_clock": round(need / sec / 1e9 / (256 * SPEC_CLOCK_GHZ), 4),
                                 "vmem_insts_per_ray": round(pmc.get("vmem_insts_per_ray") or 0.0, 2)}
+        if pmc.get("td_busy_cycles_per_ray") and pmc.get("clock_ghz"):
+            # the data-return unit (one TD per CU) returns every VMEM wave-instruction's data in
+            # order (16 cycles per 16-B-per-lane load) and waits for the L1 on a miss; r06 counters
+            # put it at ~0.99 busy, about half of it waiting on L1 misses (TD_TC_STALL)
+            need = pmc["td_busy_cycles_per_ray"] * rays_launch
+            td = {"achieved": need / sec / 1e9, "peak": 256 * pmc["clock_ghz"], "unit": "G TD-cycles/s",
+                  "how": "PMC TD_TD_BUSY_sum per traced ray x rays per launch / HIP-event launch time, over 256 "
+                         "TDs (one per CU) at the GRBM-measured clock",
+                  "frac_at_spec_clock": round(need / sec / 1e9 / (256 * SPEC_CLOCK_GHZ), 4)}
+            if pmc.get("td_tc_stall_cycles_per_ray"):
+                td["tc_stall_share"] = round(pmc["td_tc_stall_cycles_per_ray"] / pmc["td_busy_cycles_per_ray"], 4)
+            if pmc.get("tcp_accesses_per_ray"):
+                td["tcp_accesses_per_ray"] = round(pmc["tcp_accesses_per_ray"], 2)
+            if pmc.get("tcp_l2_reads_per_ray") and pmc.get("tcp_accesses_per_ray"):
+                td["l1_hit_rate"] = round(1.0 - pmc["tcp_l2_reads_per_ray"] / pmc["tcp_accesses_per_ray"], 4)
+            cands["td-busy"] = td
     for c in cands.values():
         c["frac"] = round(c["achieved"] / c["peak"], 4)
         c["achieved"] = round(c["achieved"], 2)

@@ -13,6 +13,7 @@ stream, so frame k's gather overlaps frame k+1's rendering.
 from __future__ import annotations
 
 import ctypes as C
+import time
 
 import numpy as np
 
@@ -75,8 +76,11 @@ class FrameGather:
         import torch.distributed as dist
 
         if local.device.type != "cuda":
-            return GatherHandle(self.gather(local), None)
+            t0 = time.perf_counter()
+            full = self.gather(local)
+            return GatherHandle(full, None, host_ms=(time.perf_counter() - t0) * 1e3)
         if dist.get_backend() != "nccl":  # rehearsal over gloo: stage through host memory, synchronously
+            t0 = time.perf_counter()
             host = FrameGather.__new__(FrameGather)
             host.__dict__.update(self.__dict__)
             host.send, host.maps = self.send.cpu(), [m.cpu() for m in self.maps]
@@ -85,26 +89,28 @@ class FrameGather:
             full = host.gather(local.cpu())
             if self.rank == 0:
                 self.full.copy_(full)
-                return GatherHandle(self.full, None)
-            return GatherHandle(None, None)
+            return GatherHandle(self.full if self.rank == 0 else None, None,
+                                host_ms=(time.perf_counter() - t0) * 1e3)
         if self._side is None:
             self._side = torch.cuda.Stream(device=local.device)
             self._copied = torch.cuda.Event()
         stream = stream if stream is not None else torch.cuda.current_stream(local.device)
         ready = torch.cuda.Event()
         ready.record(stream)
-        done = torch.cuda.Event()
+        done = torch.cuda.Event(enable_timing=True)
+        start = torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
             self.send[: self.n_local].copy_(local)
             self._copied.record(self._side)
+            start.record(self._side)  # the collective + scatter, timed on the side stream
             dist.gather(self.send, self.recv, dst=0)
             if self.rank == 0:
                 for r in range(self.world):
                     self.full.index_copy_(0, self.maps[r], self.recv[r][: self.counts[r]])
             done.record(self._side)
         stream.wait_event(self._copied)
-        return GatherHandle(self.full if self.rank == 0 else None, done)
+        return GatherHandle(self.full if self.rank == 0 else None, done, start=start)
 
     def wait(self):
         """Block the host until every gather_async() so far has completed."""
@@ -116,8 +122,19 @@ class GatherHandle:
     """Completion of one FrameGather.gather_async(): the rank-0 image is valid on a
     stream after wait(stream), on the host after synchronize()."""
 
-    def __init__(self, full, event):
+    def __init__(self, full, event, start=None, host_ms=None):
         self._full, self._event = full, event
+        self._start, self._host_ms = start, host_ms
+
+    def elapsed_ms(self):
+        """Time of this gather: side-stream HIP events around the collective and the scatter
+        (RCCL), or the host time of the synchronous path (gloo / CPU tensors)."""
+        if self._host_ms is not None:
+            return self._host_ms
+        if self._start is None or self._event is None:
+            return None
+        self._event.synchronize()
+        return self._start.elapsed_time(self._event)
 
     def wait(self, stream=None):
         """Make `stream` (default: the current stream) wait for the scatter; returns

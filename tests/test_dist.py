@@ -91,3 +91,44 @@ def test_gather_async_on_gpu_single_rank():
         assert torch.equal(full[:, 3], torch.ones_like(pix))
     finally:
         dist.destroy_process_group()
+
+
+def _report_worker(rank, world, port, out_path):
+    import json
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a real gather per "step" through FrameGather's synchronous (gloo) path, timed by its handle
+    g = FrameGather(64, 48, 16, rank, world, "cpu")
+    local = torch.zeros((g.n_local, 4), dtype=torch.float32)
+    handles = [g.gather_async(local) for _ in range(3)]
+    per_rank, comm = bench.rank_report(0.5 + 0.1 * rank, 1000 * (rank + 1), [h.elapsed_ms() for h in handles], "cpu")
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump({"ranks": per_rank, "comm": comm}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_rank_report_names_every_rank(tmp_path, world):
+    """bench.py --gpus N (N > 1) reports each rank's elapsed time, rays and gather time per step
+    and the communicator's world size, so a scaling run shows which rank was slow and that the
+    collective held N ranks."""
+    import json
+
+    out = str(tmp_path / "report.json")
+    mp.spawn(_report_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    rep = json.load(open(out))
+    assert rep["comm"]["world_size"] == world and rep["comm"]["backend"] == "gloo"
+    assert rep["comm"]["ranks_reporting"] == world and rep["comm"]["rccl_version"]
+    assert [r["rank"] for r in rep["ranks"]] == list(range(world))
+    for r in rep["ranks"]:
+        assert r["elapsed_ms"] == pytest.approx(500 + 100 * r["rank"])
+        assert r["rays"] == 1000 * (r["rank"] + 1)
+        assert r["gather_ms_per_step"] is not None and r["gather_ms_per_step"] >= 0

@@ -10,5 +10,8 @@ for n in ${RANKS:-2 8}; do
     --dump gpurun_out/frame$n.npy > gpurun_out/r$n.log 2>&1 || exit 1
   python -c "
 import numpy as np; a=np.load('gpurun_out/frame1.npy'); b=np.load('gpurun_out/frame$n.npy')
-print('ranks $n: frame bit-identical to 1 GPU:', a.shape == b.shape and (a.view(np.uint32) == b.view(np.uint32)).all())"
+print('ranks $n: frame bit-identical to 1 GPU:', a.shape == b.shape and (a.view(np.uint32) == b.view(np.uint32)).all())
+import json; l=[json.loads(x) for x in open('gpurun_out/r$n.log') if x.startswith('{')][-1]
+print('ranks $n: comm', json.dumps(l['comm'])); print('ranks $n: per rank', json.dumps(l['ranks']))"
 done
+rm -f gpurun_out/frame*.npy

@@ -98,6 +98,15 @@ def traffic_json(root, kernels, out_path, note=""):
            "ta_busy_cycles_per_ray": total("TA_TA_BUSY_sum") / n_rays if n_rays and pooled("TA_TA_BUSY_sum") else None,
            "vmem_insts_per_ray": total("TA_TOTAL_WAVEFRONTS_sum") / n_rays
            if n_rays and pooled("TA_TOTAL_WAVEFRONTS_sum") else None,
+           # the data-return unit (TD, one per CU) and the L1 (TCP) it waits on (r06: the traversal's
+           # binding unit, busy ~0.99 of the cycles, about half of them stalled on L1 misses)
+           "td_busy_cycles_per_ray": total("TD_TD_BUSY_sum") / n_rays if n_rays and pooled("TD_TD_BUSY_sum") else None,
+           "td_tc_stall_cycles_per_ray": total("TD_TC_STALL_sum") / n_rays
+           if n_rays and pooled("TD_TC_STALL_sum") else None,
+           "tcp_accesses_per_ray": total("TCP_TOTAL_CACHE_ACCESSES_sum") / n_rays
+           if n_rays and pooled("TCP_TOTAL_CACHE_ACCESSES_sum") else None,
+           "tcp_l2_reads_per_ray": total("TCP_TCC_READ_REQ_sum") / n_rays
+           if n_rays and pooled("TCP_TCC_READ_REQ_sum") else None,
            "dispatches": len(d),
            "simd_efficiency": simd,
            "note": note}
