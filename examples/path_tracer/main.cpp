@@ -141,10 +141,17 @@ static int BenchWaste(Pupil::System &system, Pupil::pt::PTPass &pass, const char
         }
         if (hipDeviceSynchronize() != hipSuccess || !pass.Stats(b)) return 1;
         char rec[256];
-        std::snprintf(rec, sizeof(rec), "%s{\"k\": %d, \"rays\": %llu, \"frames_dropped_by_move\": %llu, \"onrun_ms_max\": %.3f}",
+        std::snprintf(rec, sizeof(rec), "%s{\"k\": %d, \"rays\": %llu, \"frames_dropped_by_move\": %llu, \"onrun_ms_max\": %.3f",
                       i ? ", " : "", ks[i], (unsigned long long)(b.rays_traced_total - a.rays_traced_total),
                       (unsigned long long)b.frames_in_flight, pct(ms, 1.0));
         out += rec;
+        // the first OnRuns after the move, one by one (where the pipeline refills)
+        out += ", \"onrun_ms_first\": [";
+        for (size_t j = 0; j < ms.size() && j < 12; j++) {
+            std::snprintf(rec, sizeof(rec), "%s%.3f", j ? ", " : "", ms[j]);
+            out += rec;
+        }
+        out += "]}";
     }
     move();
     system.Run(1);  // the last stretch's frames in flight are dropped here

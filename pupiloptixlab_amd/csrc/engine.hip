@@ -119,12 +119,24 @@ struct pupil_pt {
         uint32_t frames, consumed;    // frames in the group; accumulated (rendered) so far
     };
     std::vector<PipeFrame> pipe;      // in flight, oldest first
+    // an iteration split over two renders (frame-group pacing, render_pipelined): the trace half
+    // ran, the shade half is due at the start of the next render
+    struct HalfIter {
+        bool had, inject;
+        PipeFrame nf;
+        uint32_t nfp;
+    };
+    HalfIter half{};
+    bool half_pending = false;
+    bool pipe_split = true;           // PUPIL_PIPE_SPLIT=0: whole iterations only (A/B)
+    uint32_t pipe_group_max = 2;      // PUPIL_PIPE_GROUP_MAX: frames per group at most (the latency bound)
+    uint32_t pipe_ramp = 1;           // PUPIL_PIPE_RAMP: groups one render may start ahead (0 = no limit)
     uint32_t pipe_slots = 0;          // K of the ring in use
     size_t pipe_np = 0;               // paths per slot
     uint32_t pipe_key[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // w, h, tile size, rank, world, spp, depth, local pixels, G
     size_t pipe_cap = 0;              // paths per ring slot (G frames)
     // PUPIL_PIPE_GROUP_PATHS: renders of fewer paths batch G = ceil(this / paths) frames per slot
-    double pipe_group_paths = 8e6;
+    double pipe_group_paths = 4e6;
     // renders that start no frame ahead (a moving camera) with at most this many paths run as one
     // persistent launch per frame (pt_frame.hip); PUPIL_FRAME_PATHS, 0 = never.  Moving-camera
     // OnRuns at 1080p (r05 shard probe): one rank of 8 (260 k paths) 7.40 vs 8.47 ms per 8 OnRuns
@@ -241,6 +253,7 @@ struct pupil_pt {
         q.bins = q.nxsh = q.hist = nullptr;
         cap = 0;
         pipe.clear();
+        half_pending = false;
         pipe_valid = false;
     }
     ~pupil_pt() {
@@ -605,7 +618,8 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
             return e && std::atoi(e) != 0;
         }();
         if (launch->spp == 1 || group_all)
-            G = (uint32_t)std::min(64.0, std::max(1.0, std::ceil(pt->pipe_group_paths / (double)np)));
+            G = (uint32_t)std::min((double)pt->pipe_group_max,
+                                   std::max(1.0, std::ceil(pt->pipe_group_paths / (double)np)));
         K = pt->pipe_limit ? std::min(pt->pipe_limit, D) : D;
         constexpr double kPathBytes = 8 * 16 + 2 + 4 + 8 + 1;  // PathState + bins + nxsh + partition scratch
         K = std::min<uint32_t>(K, (uint32_t)std::max(1.0, std::floor(pt->pipe_budget / ((double)G * np * kPathBytes))));
@@ -672,6 +686,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
             pt->ring_fresh = false;
         }
         pt->pipe.clear();
+        pt->half_pending = false;  // an iteration split over the last render and this one is dropped
         pt->pipe_run = continued ? pt->pipe_run + 1 : 0;
         pt->pipe_slots = K;
         pt->pipe_np = np;
@@ -711,8 +726,6 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         pt->frame_launches++;
         return PUPIL_OK;
     }
-    // iterations this render needs: none when an earlier render completed its frame
-    const uint32_t L = pt->pipe.empty() ? D : D - pt->pipe.front().phases;
     // AOV scratch of ring slot `slot`, frame `f` of its group: 7 floats per local pixel
     auto scratch = [&](uint32_t slot, uint32_t f) { return pt->aov_scratch + ((size_t)slot * G + f) * 7 * nl; };
     uint64_t started = 0;
@@ -720,28 +733,47 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
     // once no path is left (all of them missed, were absorbed or were terminated by RR)
     const bool deep_exit = D > 64 && K == 1;
     pt->snap_taken = false;
-    for (uint32_t it = 0; it < L; it++) {
-        const bool had = !pt->pipe.empty();
+    // One iteration in two halves: (a) start a frame group if due, list the rays the previous
+    // shade spawned and trace them (with the new group's camera rays); (b) partition by
+    // material, shade.  Frame-group pacing runs (a) at the end of the render before the one
+    // that needs the iteration (below), (b) at that render's start.
+    using Half = pupil_pt::HalfIter;
+    // a render that starts on an empty pipeline (the first speculating render after a reset: it
+    // traces its own frame from the camera rays) starts at most PUPIL_PIPE_RAMP groups ahead;
+    // the renders after it fill the ring as before (one group more per iteration they run)
+    uint32_t ahead_started = 0;
+    bool fresh_start = false;
+    auto trace_half = [&](uint32_t it, uint32_t L_it, uint32_t run) -> int {
+        Half h{};
+        h.had = !pt->pipe.empty();
         // start a frame group: this render's own on an empty pipeline (one frame unless
         // speculating), else the next one ahead in the last run + 1 iterations while a slot is free
-        const bool inject = !had || (speculate && pt->pipe.size() < K && it + pt->pipe_run + 1 >= L);
-        pupil_pt::PipeFrame nf{0u, launch->random_seed, 0u, false, speculate ? G : 1u, 0u};
-        if (inject && had) {
-            nf.slot = (pt->pipe.back().slot + 1) % K;
-            nf.seed = pt->pipe.back().seed + pt->pipe.back().frames * fp.spp;
+        if (!h.had) fresh_start = true;
+        h.inject = !h.had || (speculate && pt->pipe.size() < K && it + run + 1 >= L_it &&
+                              (pt->pipe_ramp == 0 || !fresh_start || ahead_started < pt->pipe_ramp));
+        if (h.inject && h.had) ahead_started++;
+        // a group started on an empty pipeline (the render's own frame: after a reset, the first
+        // speculating render) holds one frame when the ramp is limited, so that render traces
+        // its own frame and at most PUPIL_PIPE_RAMP groups' first bounces, not G frames' worth
+        // (r06 pacing: the heaviest OnRun after the camera stops)
+        h.nf = pupil_pt::PipeFrame{0u, launch->random_seed, 0u, false,
+                                   speculate && (h.had || pt->pipe_ramp == 0) ? G : 1u, 0u};
+        if (h.inject && h.had) {
+            h.nf.slot = (pt->pipe.back().slot + 1) % K;
+            h.nf.seed = pt->pipe.back().seed + pt->pipe.back().frames * fp.spp;
         }
-        nf.aov_scratch = had || nf.frames > 1;  // AOVs wait in the slot's scratch until the frame's render
-        const uint32_t nfp = (uint32_t)(nf.frames * np);  // paths of the new group
-        const uint32_t gspp = nf.frames * fp.spp;         // its samples per pixel
+        h.nf.aov_scratch = h.had || h.nf.frames > 1;  // AOVs wait in the slot's scratch until the frame's render
+        h.nfp = (uint32_t)(h.nf.frames * np);          // paths of the new group
+        const uint32_t gspp = h.nf.frames * fp.spp;    // its samples per pixel
         const uint32_t interleave = interleave0 && gspp > 1 ? gspp : 0u;
-        if (inject) {
+        if (h.inject) {
             FrameParams fg = fp;
-            fg.seed0 = nf.seed;
-            fg.num_paths = nfp;
-            launch_generate(pt->sc, fg, cx.view(nf.slot, cap_paths), s, !pt->fresh());
-            started += nfp;
+            fg.seed0 = h.nf.seed;
+            fg.num_paths = h.nfp;
+            launch_generate(pt->sc, fg, cx.view(h.nf.slot, cap_paths), s, !pt->fresh());
+            started += h.nfp;
         }
-        if (had) {
+        if (h.had) {
             // the rays the previous iteration's shade spawned, over the slots in use, in
             // increasing path id: next (bit 0) and shadow (bit 1) lists -> q.nxsh
             const uint32_t tag = pt->pipe_gen % 63u + 1u;
@@ -753,35 +785,40 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
                 uint32_t c[2] = {1, 1};
                 HIP_TRY(hipMemcpyAsync(c, q.counts + kCntNext, sizeof(c), hipMemcpyDeviceToHost, s));
                 HIP_TRY(hipStreamSynchronize(s));
-                if (c[0] == 0 && c[1] == 0) break;  // nothing left to trace or shade: the frame is complete
+                if (c[0] == 0 && c[1] == 0) return 1;  // nothing left to trace or shade: the frame is complete
             }
             cx.ev0(1);
             cx.tail_slot();
-            if (inject)  // + the new group's camera rays, dequeued first in every chunk (pixel-major)
-                launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s, nfp, 0u,
-                                   (uint32_t)(nf.slot * cap_paths), interleave, nl);
+            if (h.inject)  // + the new group's camera rays, dequeued first in every chunk (pixel-major)
+                launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s, h.nfp, 0u,
+                                   (uint32_t)(h.nf.slot * cap_paths), interleave, nl);
             else
                 launch_trace_mixed(pt->sc, ring, q, pt->ovf, pt->ovf_threads, cx.tsp(), s);
             cx.ev1();
         } else {
             cx.ev0(0);
             cx.tail_slot();
-            launch_extend(pt->sc, cx.view(nf.slot, cap_paths), q, nullptr, nullptr, nfp, pt->ovf, pt->ovf_threads,
+            launch_extend(pt->sc, cx.view(h.nf.slot, cap_paths), q, nullptr, nullptr, h.nfp, pt->ovf, pt->ovf_threads,
                           cx.tsp(), s, interleave, nl);
             cx.ev1();
         }
-        if (inject) {  // the group is in flight from here (ring_end covers it)
-            nf.phases = 0;
-            pt->pipe.push_back(nf);
+        if (h.inject) {  // the group is in flight from here (ring_end covers it)
+            h.nf.phases = 0;
+            pt->pipe.push_back(h.nf);
         }
+        pt->half = h;
+        return 0;
+    };
+    auto shade_half = [&]() -> int {
+        const Half h = pt->half;
         const uint32_t nring = ring_end();
         if (!pt->shade_list)  // material bins of every path traced in this iteration -> q.bins
             launch_partition(ring.mbin, nring, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
                              q.counts + kStartBins, q.counts + kScratch, nullptr, s);
         FrameParams fs = fp;
         fs.group = G;  // AOV frame of a sample: its group frame (samples per ring slot = G spp)
-        if (inject && nf.aov_scratch) {  // AOVs of frames ahead wait in their slot's scratch
-            fs.albedo = scratch(nf.slot, 0);
+        if (h.inject && h.nf.aov_scratch) {  // AOVs of frames ahead wait in their slot's scratch
+            fs.albedo = scratch(h.nf.slot, 0);
             fs.normal = fs.albedo + 3 * (size_t)nl;
             fs.test = fs.albedo + 6 * (size_t)nl;
             fs.aov_local = 1;
@@ -789,16 +826,33 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         }
         if (D > 63) HIP_TRY(hipMemsetAsync(ring.sflags, 0, nring, s));  // K = 1: tags would alias
         const uint32_t wtag = (pt->pipe_gen + 1u) % 63u + 1u;
-        const ShadeList list = !pt->shade_list ? kShadeBins : (had ? (inject ? kShadeNextRange : kShadeNext) : kShadeAll);
+        const ShadeList list =
+            !pt->shade_list ? kShadeBins : (h.had ? (h.inject ? kShadeNextRange : kShadeNext) : kShadeAll);
         uint64_t live = 0;  // paths the launch may list
         for (const auto &g : pt->pipe) live += (uint64_t)g.frames * np;
         const uint32_t max_count = (uint32_t)std::min<uint64_t>(nring, live);
         cx.ev0(2);
-        launch_shade(pt->sc, fs, ring, q, wtag, s, list, (uint32_t)(nf.slot * cap_paths), inject ? nfp : 0u, max_count,
-                     pt->fresh(), nf.seed);
+        launch_shade(pt->sc, fs, ring, q, wtag, s, list, (uint32_t)(h.nf.slot * cap_paths), h.inject ? h.nfp : 0u,
+                     max_count, pt->fresh(), h.nf.seed);
         cx.ev1();
         pt->pipe_gen++;
         for (auto &f : pt->pipe) f.phases++;
+        return 0;
+    };
+    // the shade half of an iteration whose trace half the previous render ran (a reset above
+    // dropped it with the frames it belonged to)
+    if (pt->half_pending) {
+        pt->half_pending = false;
+        if (!reset)
+            if (const int rc = shade_half()) return rc;
+    }
+    // iterations this render needs: none when an earlier render completed its frame
+    const uint32_t L = pt->pipe.empty() ? D : D - pt->pipe.front().phases;
+    for (uint32_t it = 0; it < L; it++) {
+        const int rc = trace_half(it, L, pt->pipe_run);
+        if (rc == 1) break;  // depth > 64: nothing left
+        if (rc) return rc;
+        if (const int rs = shade_half()) return rs;
     }
     // this render's frame is complete: accumulate it; the group's slot is free once all
     // its frames are accumulated
@@ -808,6 +862,17 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
     launch_accumulate(fp, cx.view(g.slot, cap_paths, (size_t)f * np), g.aov_scratch ? scratch(g.slot, f) : nullptr,
                       true, s);
     if (++g.consumed == g.frames) pt->pipe.erase(pt->pipe.begin());
+    // Frame-group pacing (r06): the render that displays a group's last frame, and would
+    // otherwise do no traversal, runs the trace half of the iteration the next render needs;
+    // that render starts with the shade half.  With G = 2 the traversal and the shade of every
+    // iteration land in different OnRuns (~0.8 / 0.2 of an iteration) instead of one OnRun
+    // doing all of it and the next none.  Speculative like the frames ahead: a reset drops it.
+    if (pt->pipe_split && speculate && G > 1 && L == 0 && !pt->pipe.empty() && pt->pipe.front().phases < D) {
+        const uint32_t L_next = D - pt->pipe.front().phases;
+        const int rc = trace_half(0, L_next, pt->pipe_run + 1);
+        if (rc < 0) return rc;
+        pt->half_pending = rc == 0;
+    }
     pt->pipe_next_seed = launch->random_seed + fp.spp;
     pt->last_iters = L;
     pt->last_primary = started;
@@ -1052,6 +1117,9 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (const char *g = std::getenv("PUPIL_PIPE_GB")) pt->pipe_budget = std::max(0.0, std::atof(g)) * 1e9;
     if (const char *g = std::getenv("PUPIL_PIPE_PATHS")) pt->pipe_paths = std::max(1.0, std::atof(g));
     if (const char *g = std::getenv("PUPIL_PIPE_GROUP_PATHS")) pt->pipe_group_paths = std::max(1.0, std::atof(g));
+    if (const char *g = std::getenv("PUPIL_PIPE_GROUP_MAX")) pt->pipe_group_max = (uint32_t)std::min(64, std::max(1, std::atoi(g)));
+    if (const char *g = std::getenv("PUPIL_PIPE_SPLIT")) pt->pipe_split = std::atoi(g) != 0;
+    if (const char *g = std::getenv("PUPIL_PIPE_RAMP")) pt->pipe_ramp = (uint32_t)std::max(0, std::atoi(g));
     if (const char *g = std::getenv("PUPIL_FRAME_PATHS")) pt->frame_paths = std::max(0.0, std::atof(g));
     sc.trace_node_min = 8;  // node phase ends below 8 active lanes (7 waves: 8 and 12 beat 4 by 1.5 %; 2 is slower)
     if (const char *r = std::getenv("PUPIL_NODE_MIN")) sc.trace_node_min = (uint32_t)std::min(64, std::max(1, std::atoi(r)));

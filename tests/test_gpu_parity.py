@@ -556,7 +556,7 @@ def test_camera_change_uploads_new_sensor():
 
 
 PIPE_CASES = ["flat", "two_level", "two_level_world", "bins", "batched", "hint", "deep", "pipe3", "tiles", "group",
-              "group_tiles", "group_bins", "group_hint"]
+              "group_tiles", "group_bins", "group_hint", "group2", "group2_deep", "group_nosplit"]
 
 
 @pytest.mark.parametrize("case", PIPE_CASES)
@@ -571,14 +571,21 @@ def test_pipelined_onrun_sequence(case, monkeypatch):
     ring), two-level structures, batched renders (PUPIL_AHEAD=2 / the hint), a ring
     capped below max_depth (PUPIL_PIPE=3) and tile-sharded compact buffers.  The group
     cases batch 4 consecutive frames per ring slot (small renders: PUPIL_PIPE_GROUP_PATHS),
-    so most renders only accumulate a frame an earlier render's launches completed."""
+    so most renders only accumulate a frame an earlier render's launches completed; the
+    render before the one that needs the next iteration runs its trace half, that render its
+    shade half (r06 pacing; "group2": the default two frames per group, "group_nosplit":
+    PUPIL_PIPE_SPLIT=0).  Camera moves, seed jumps and depth changes land between the halves."""
     import torch
     from pupiloptixlab_amd.pt_pass import PTPass, Events
     from pupiloptixlab_amd import world as W
 
     grouped = case.startswith("group")
     if grouped:
-        case = {"group": "flat", "group_tiles": "tiles", "group_bins": "bins", "group_hint": "hint"}[case]
+        monkeypatch.setenv("PUPIL_PIPE_GROUP_MAX", "2" if case.startswith("group2") else "4")
+        if case == "group_nosplit":
+            monkeypatch.setenv("PUPIL_PIPE_SPLIT", "0")
+        case = {"group": "flat", "group_tiles": "tiles", "group_bins": "bins", "group_hint": "hint", "group2": "flat",
+                "group2_deep": "deep", "group_nosplit": "flat"}[case]
     if case == "two_level":
         monkeypatch.setenv("PUPIL_ACCEL", "two_level")
         monkeypatch.setenv("PUPIL_TL_MODE", "object")
