@@ -129,7 +129,10 @@ struct pupil_pt {
     HalfIter half{};
     bool half_pending = false;
     bool pipe_split = true;           // PUPIL_PIPE_SPLIT=0: whole iterations only (A/B)
-    uint32_t pipe_group_max = 2;      // PUPIL_PIPE_GROUP_MAX: frames per group at most (the latency bound)
+    // PUPIL_PIPE_GROUP_MAX: frames per group at most.  The latency bound is the group's paths
+    // (PUPIL_PIPE_GROUP_PATHS, 4 M: two 1080p frames), so the heaviest OnRun carries the same
+    // work at any tile share (profiles/r06_shard_probe_onrun.txt); 2 caps it at N = 1 sizes too
+    uint32_t pipe_group_max = 64;
     uint32_t pipe_ramp = 1;           // PUPIL_PIPE_RAMP: groups one render may start ahead (0 = no limit)
     uint32_t pipe_slots = 0;          // K of the ring in use
     size_t pipe_np = 0;               // paths per slot

@@ -38,6 +38,11 @@ constexpr uint32_t kQKindShadow = 0x80000000u;  // shadow ray of the path's curr
 constexpr uint32_t kQPath = 0x7FFFFFFFu;
 constexpr uint32_t kFrameQ = 128;  // entries per wave and queue (a wave owns at most 64 paths, 2 rays each)
 constexpr uint32_t kFrameWaves = kTraceBlock / 64;
+// waves per SIMD of the one-launch frame kernel (its registers: trace + shade state); A/B builds
+#ifndef PUPIL_FRAME_WAVES
+#define PUPIL_FRAME_WAVES 4
+#endif
+constexpr uint32_t kFrameWavesPerSimd = PUPIL_FRAME_WAVES;
 
 struct FrameJob {
     uint32_t *work;      // kWorkKind counters (XCD-sharded dequeue heads + exit counters), zero at launch
@@ -99,7 +104,7 @@ struct WaveQueue {
 };
 
 template <uint32_t MAT>
-__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_frame(
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kFrameWavesPerSimd))) void k_frame(
     DeviceScene sc, FrameParams fp, PathState ps, FrameJob job, int *ovf, uint32_t ovf_threads) {
     constexpr float kInf = __builtin_huge_valf();
     __shared__ int s_ring[kRing * kTraceBlock];
@@ -307,7 +312,7 @@ bool frame_kernel_supported(const DeviceScene &sc) { return !(sc.two_level && !s
 void launch_frame(const DeviceScene &sc, const FrameParams &fp, const PathState &ps, uint32_t *work,
                   unsigned long long *ray_cum, int *ovf, uint32_t ovf_threads, uint32_t interleave_spp, hipStream_t s) {
     FrameJob job{work, fp.num_paths, sc.trace_refill, sc.trace_node_min, interleave_spp, fp.num_local, ray_cum};
-    const uint32_t resident = sc.num_cus * 4u * 4u / kFrameWaves;
+    const uint32_t resident = sc.num_cus * 4u * kFrameWavesPerSimd / kFrameWaves;
     const uint32_t by_paths = (fp.num_paths + kTraceBlock - 1) / kTraceBlock;
     const uint32_t blocks = std::min(ovf_threads / kTraceBlock, std::max(1u, std::min(resident, by_paths)));
     switch (sc.single_bin) {
