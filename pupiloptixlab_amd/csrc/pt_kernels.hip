@@ -159,15 +159,27 @@ __global__ __launch_bounds__(kShadeBlock) void k_accumulate(FrameParams fp, Path
         if (fp.test) fp.test[out] = aov_src[6 * n + l];
     }
     vec3 acc = f3(fp.accum[out]);
-    for (uint32_t s = 0; s < fp.spp; s++) {
-        if (clear_flags) ps.sflags[(size_t)s * fp.num_local + l] = 0u;
-        vec3 L = f3(ps.rad[(size_t)s * fp.num_local + l]);
-        const uint32_t cnt = fp.cnt0 + (fp.accumulate ? s : 0u);
-        if (fp.accumulate && cnt > 0) {  // main.cu:187-191
-            const float t = 1.f / ((float)cnt + 1.f);
-            L = lerp(acc, L, t);
+    // the samples' radiance 8 at a time: their loads issued together (one memory latency per
+    // batch, not per sample); the lerps run in sample order as before
+    constexpr uint32_t kBatch = 8;
+    for (uint32_t s0 = 0; s0 < fp.spp; s0 += kBatch) {
+        float4 rad[kBatch];
+#pragma unroll
+        for (uint32_t j = 0; j < kBatch; j++)
+            if (s0 + j < fp.spp) rad[j] = ps.rad[(size_t)(s0 + j) * fp.num_local + l];
+#pragma unroll
+        for (uint32_t j = 0; j < kBatch; j++) {
+            const uint32_t s = s0 + j;
+            if (s >= fp.spp) break;
+            if (clear_flags) ps.sflags[(size_t)s * fp.num_local + l] = 0u;
+            vec3 L = f3(rad[j]);
+            const uint32_t cnt = fp.cnt0 + (fp.accumulate ? s : 0u);
+            if (fp.accumulate && cnt > 0) {  // main.cu:187-191
+                const float t = 1.f / ((float)cnt + 1.f);
+                L = lerp(acc, L, t);
+            }
+            acc = L;
         }
-        acc = L;
     }
     fp.accum[out] = f4(acc, 1.f);
     if (fp.frame) fp.frame[out] = f4(acc, 1.f);
