@@ -578,6 +578,8 @@ def roofline(args, st_bytes, timed):
                 td["tc_stall_share"] = round(pmc["td_tc_stall_cycles_per_ray"] / pmc["td_busy_cycles_per_ray"], 4)
             if pmc.get("tcp_accesses_per_ray"):
                 td["tcp_accesses_per_ray"] = round(pmc["tcp_accesses_per_ray"], 2)
+            if pmc.get("td_busy_frac_under_pmc"):  # busy fraction inside the PMC passes (no live timing)
+                td["busy_frac_under_pmc"] = round(pmc["td_busy_frac_under_pmc"], 4)
             if pmc.get("tcp_l2_reads_per_ray") and pmc.get("tcp_accesses_per_ray"):
                 td["l1_hit_rate"] = round(1.0 - pmc["tcp_l2_reads_per_ray"] / pmc["tcp_accesses_per_ray"], 4)
             cands["td-busy"] = td

@@ -103,6 +103,12 @@ def traffic_json(root, kernels, out_path, note=""):
            "td_busy_cycles_per_ray": total("TD_TD_BUSY_sum") / n_rays if n_rays and pooled("TD_TD_BUSY_sum") else None,
            "td_tc_stall_cycles_per_ray": total("TD_TC_STALL_sum") / n_rays
            if n_rays and pooled("TD_TC_STALL_sum") else None,
+           # the same within the PMC passes themselves: TD busy over 256 TDs and the per-XCD cycles
+           # (per-dispatch averages of the TD pass and of the GRBM pass; no live launch time involved)
+           "td_busy_frac_under_pmc": pooled("TD_TD_BUSY_sum") / 256.0 / (grbm / 8.0)
+           if grbm and pooled("TD_TD_BUSY_sum") else None,
+           "td_tc_stall_frac_under_pmc": pooled("TD_TC_STALL_sum") / 256.0 / (grbm / 8.0)
+           if grbm and pooled("TD_TC_STALL_sum") else None,
            "tcp_accesses_per_ray": total("TCP_TOTAL_CACHE_ACCESSES_sum") / n_rays
            if n_rays and pooled("TCP_TOTAL_CACHE_ACCESSES_sum") else None,
            "tcp_l2_reads_per_ray": total("TCP_TCC_READ_REQ_sum") / n_rays
