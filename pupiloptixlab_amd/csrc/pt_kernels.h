@@ -29,10 +29,17 @@ constexpr bool kCoopFetch = PUPIL_COOP != 0;
 #define PUPIL_COOP_CHUNKS 1
 #endif
 constexpr int kCoopChunks = PUPIL_COOP_CHUNKS;
+// distance stack in k_trace4 (flat kernels): every LDS entry carries its entry distance and pops
+// skip entries already beyond tmax (pt_traverse.h pop_live); the distances take a second LDS
+// column, so it pairs with a smaller ring (PUPIL_TRACE_RING=8)
+#ifndef PUPIL_DIST_STACK
+#define PUPIL_DIST_STACK 0
+#endif
+constexpr bool kDistStack = PUPIL_DIST_STACK != 0;
 // k_trace4's LDS ring: the cooperative fetch's staging (1 KiB + 256 B per wave and chunk) comes
 // out of the ring so 14 blocks still fit a CU's 160 KiB
 #ifndef PUPIL_TRACE_RING
-#define PUPIL_TRACE_RING (PUPIL_COOP ? 13 : 16)
+#define PUPIL_TRACE_RING (PUPIL_COOP ? 13 : (PUPIL_DIST_STACK ? 8 : 16))
 #endif
 constexpr int kTraceRing = PUPIL_TRACE_RING;
 static_assert(kTraceRing >= 8 && kTraceRing <= kRing, "trace ring");

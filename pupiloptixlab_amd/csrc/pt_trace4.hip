@@ -66,12 +66,13 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     // mixed launches may carry the next render's camera rays (render-ahead, TraceJob::ahead_off)
     const uint32_t n_ahead = MODE == kModeMixedAhead ? job.static_count : 0u;
     const uint32_t count = kMixed ? n_next + q.counts[kCntShadow] : (job.count_ptr ? *job.count_ptr : job.static_count);
-    LinStackT<RING, COOP ? kTraceStackOvf : kStackOvf> st;
+    LinStackT<RING, RING == kRing ? kStackOvf : kTraceStackOvf> st;
     st.lds = s_ring + threadIdx.x;
     st.ovf_blk = ovf + blockIdx.x * blockDim.x;
     st.lds0 = s_ring;
     st.ovf_stride = ovf_threads;
-    if (STATS) st.tcol = s_tst + threadIdx.x;
+    constexpr bool kDist = kDistStack && !TL;
+    if (STATS || kDist) st.tcol = s_tst + threadIdx.x;
     st.reset();
     CoopFetch<kCoopChunks> cf;
     if (COOP) {
@@ -108,6 +109,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
     uint32_t best_key = 0;
     RayPre r{};
     float tmin = MODE == kModeRays ? 0.f : 0.001f, tmax = 0.f;  // tmin: a constant outside kModeRays
+    auto popn = [&]() { return kDist ? st.pop_live(tmax) : st.pop(); };
     // state read only at a hit update or at the retire lives in LDS (s_aux), not in VGPRs:
     // the path id and the best hit's barycentrics
     float &b1 = s_aux[threadIdx.x];
@@ -268,7 +270,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             n_nohit += t[0] == kInf ? 1u : 0u;
         }
         if (t[0] == kInf) {
-            node = st.pop();
+            node = popn();
             if (STATS) t_node = st.tpop;
         } else {
             node = l[0];
@@ -276,11 +278,11 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
             st.reserve3();
             st.push3t(t[1], t[2], t[3], t[2] != kInf, t[3] != kInf);
             st.push3(l[1], l[2], l[3], t[1] != kInf, t[2] != kInf, t[3] != kInf);
-            if (node == kEmptyLink) node = st.pop();  // degenerate child boxes only (LinStack)
+            if (node == kEmptyLink) node = popn();  // degenerate child boxes only (LinStack)
         }
         if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
             leaf = node;
-            node = st.pop();
+            node = popn();
             if (STATS) t_node = st.tpop;
         }
         };
@@ -358,7 +360,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     break;
                 }
                 leaf = node;
-                if (node < 0) node = st.pop();
+                if (node < 0) node = popn();
             }
             if (TL && node == kReturnLink && leaf >= 0 && !(any && found)) {  // BLAS exhausted: back to the TLAS
                 in_blas = false;
@@ -459,14 +461,14 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
 template <int MODE, bool ANY, bool STATS, bool TOP>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerSimd))) void k_trace4(
     DeviceScene sc, PathState ps, Queues q, TraceJob job, int *ovf, uint32_t ovf_threads, TraceStats stats) {
-    constexpr int ring = kCoopFetch ? kTraceRing : kRing;
+    constexpr int ring = kCoopFetch || kDistStack ? kTraceRing : kRing;
     __shared__ int s_ring[ring * kTraceBlock];
     __shared__ float s_aux[4 * kTraceBlock];
-    __shared__ float s_tst[STATS ? ring * kTraceBlock : 1];
-    __shared__ Bvh4Node s_top[kCoopFetch ? 1 : kTopNodes];
+    __shared__ float s_tst[STATS || kDistStack ? ring * kTraceBlock : 1];
+    __shared__ Bvh4Node s_top[kCoopFetch || kDistStack ? 1 : kTopNodes];
     __shared__ float4 s_coop[kCoopFetch ? (kTraceBlock / 64) * (16 + 64 * kCoopChunks) : 1];
     // the cooperative fetch replaces the LDS top-of-tree copy (its hot nodes are one shared DMA)
-    trace4_body<MODE, ANY, STATS, false, TOP && !kCoopFetch, kCoopFetch, ring>(sc, ps, q, job, ovf, ovf_threads, stats,
+    trace4_body<MODE, ANY, STATS, false, TOP && !kCoopFetch && !kDistStack, kCoopFetch, ring>(sc, ps, q, job, ovf, ovf_threads, stats,
                                                                               s_ring, s_aux, s_tst, s_top, s_coop);
 }
 

@@ -215,6 +215,15 @@ struct LinStackT {
         while (v == kEmptyLink) v = pop_raw();
         return v;
     }
+    // distance stack (PUPIL_DIST_STACK builds, tcol set): also skips entries whose conservative
+    // entry distance (the box test's lowered near plane, pushed with the link) already exceeds
+    // the ray's current tmax -- no primitive inside can be hit at t <= tmax, so the visit the
+    // pop would cause could only fail; entries reloaded from the overflow column read 0
+    __device__ __forceinline__ int pop_live(float tmax) {
+        int v = pop_raw();
+        while (v != kSentinel && (v == kEmptyLink || tpop > tmax)) v = pop_raw();
+        return v;
+    }
 };
 using LinStack = LinStackT<kRing, kStackOvf>;
 
