@@ -1010,8 +1010,27 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     DevInstance *d_insts = nullptr;
     DevMaterial *d_mats = nullptr;
     uint32_t *d_prim_inst = nullptr;
+    // the shading's prim -> instance lookup (pt_kernels.h inst_of_prim): instance starts and a
+    // guide table of at most ~8 K entries over the prim ids
+    std::vector<uint32_t> inst_first(insts.size() + 1);
+    for (size_t i = 0; i < insts.size(); i++) inst_first[i] = insts[i].prim_offset;
+    inst_first[insts.size()] = (uint32_t)prim_inst.size();
+    uint32_t guide_shift = 0;
+    while ((prim_inst.size() >> guide_shift) > 8192u) guide_shift++;
+    std::vector<uint32_t> inst_guide;
+    if (!prim_inst.empty()) {
+        const size_t nb = ((prim_inst.size() - 1) >> guide_shift) + 1;
+        inst_guide.resize(nb + 1);
+        for (size_t k = 0; k <= nb; k++)
+            inst_guide[k] = prim_inst[std::min(k << guide_shift, prim_inst.size() - 1)];
+    } else {
+        inst_guide.assign(2, 0u);
+    }
+    uint32_t *d_inst_first = nullptr, *d_inst_guide = nullptr;
     if (pt->upload(&d_insts, insts.data(), insts.size()) || pt->upload(&d_mats, mats.data(), mats.size()) ||
-        pt->upload(&d_prim_inst, prim_inst.data(), prim_inst.size()))
+        pt->upload(&d_prim_inst, prim_inst.data(), prim_inst.size()) ||
+        pt->upload(&d_inst_first, inst_first.data(), inst_first.size()) ||
+        pt->upload(&d_inst_guide, inst_guide.data(), inst_guide.size()))
         return cleanup(fail(PUPIL_ERR_OOM, "scene upload failed"));
     {
         int rc = upload_emitters(pt, scene);
@@ -1129,6 +1148,9 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
     if (nodes4_count(pt) > kMaxNodes4)
         return cleanup(fail(PUPIL_ERR_UNSUPPORTED, "BVH4 larger than 2^26 nodes (32-bit node offsets)"));
     sc.prim_inst = d_prim_inst;
+    sc.inst_first = d_inst_first;
+    sc.inst_guide = d_inst_guide;
+    sc.inst_guide_shift = guide_shift;
     sc.instances = d_insts;
     sc.materials = d_mats;
     std::memcpy(sc.camera.s2c, scene->sample_to_camera, sizeof(sc.camera.s2c));

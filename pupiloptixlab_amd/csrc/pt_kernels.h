@@ -160,6 +160,24 @@ __device__ __forceinline__ void st_ps(uint4 *a, uint4 v) {
     __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(a));
 }
 
+// The instance holding global primitive `idx`: the last instance i in the guide's range with
+// inst_first[i] <= idx (an instance without primitives shares its first id with the next one,
+// which is the one that holds it), i.e. exactly prim_inst[idx].
+#ifndef PUPIL_INST_GUIDE
+#define PUPIL_INST_GUIDE 1
+#endif
+__device__ __forceinline__ uint32_t inst_of_prim(const DeviceScene &sc, uint32_t idx) {
+    if (!PUPIL_INST_GUIDE) return sc.prim_inst[idx];
+    const uint32_t k = idx >> sc.inst_guide_shift;
+    uint32_t lo = sc.inst_guide[k], hi = sc.inst_guide[k + 1];
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1u) >> 1;
+        if (sc.inst_first[mid] <= idx) lo = mid;
+        else hi = mid - 1u;
+    }
+    return lo;
+}
+
 struct TraceStats {
     unsigned long long *counters;  // [0..1] closest-hit nodes/prims, [14..15] shadow, [2..13] diagnostics,
                                    // [16] reference shadow rays, [18] distinct node fetches,

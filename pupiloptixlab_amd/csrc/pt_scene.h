@@ -163,7 +163,14 @@ struct DeviceScene {
     uint32_t two_level;       // 1: nodes4 = TLAS over instances + object-space BLAS per shape;
                               //    prims/attrs = BLAS records, hit index = global primitive id
     const float4 *wprims;       // two-level: per-instance world-space triangle records (see accel_two_level.hip)
-    const uint32_t *prim_inst;  // global prim id -> instance
+    const uint32_t *prim_inst;  // global prim id -> instance (the builders; 4 B per primitive)
+    // global prim id -> instance for the shading (inst_of_prim): inst_first[i] = instance i's
+    // first global primitive id (num_instances + 1 entries, the last = num_prims), and a guide
+    // table over prim ids, inst_guide[k] = the instance holding prim min(k << inst_guide_shift,
+    // num_prims - 1): a few kB that stay in the L1 / L2, where prim_inst is 40 MB at config 5
+    const uint32_t *inst_first;
+    const uint32_t *inst_guide;
+    uint32_t inst_guide_shift;
     const DevInstance *instances;
     const DevMaterial *materials;
     const DevEmitter *areas;

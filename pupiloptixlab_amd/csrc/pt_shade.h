@@ -90,7 +90,7 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, c
     float4 ra[7];  // the shading record (one 128-B line)
     if (sc.two_level) {
         gprim = idx;
-        inst_id = sc.prim_inst[idx];
+        inst_id = inst_of_prim(sc, idx);
         const DevInstance &ti = sc.instances[inst_id];
         sphere = ti.kind == PUPIL_SHAPE_SPHERE;
         rec = sc.attrs + (size_t)kAttrStride * (sphere ? 0u : ti.attr_base + (idx - ti.prim_offset));

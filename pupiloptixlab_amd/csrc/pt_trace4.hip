@@ -387,7 +387,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                 // record fetch here, which would stall the wave before its next refill)
                 if (found && sc.single_bin == 0u) {
                     if (TL) {
-                        bin = sc.instances[sc.prim_inst[best_idx]].bin;
+                        bin = sc.instances[inst_of_prim(sc, best_idx)].bin;
                     } else {
                         const uint32_t mt = __float_as_uint(sc.prims[kRecF4 * best_idx + 2].w);
                         bin = (mt >= 1u && mt <= 7u) ? mt : 8u;
