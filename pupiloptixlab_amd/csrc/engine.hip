@@ -146,6 +146,7 @@ struct pupil_pt {
     // in one launch vs the stage pipeline, one of 4 (518 k) 12.86 vs 10.56, one GPU 39.7 vs 22.8
     double frame_paths = 4e5;
     bool ring_fresh = true;           // the ring was (re)allocated: its flags bytes are not yet cleared
+    uint32_t bin_mask = 0;            // material bins of the scene's instances + the miss bin (partition)
     uint32_t pipe_run = 0;            // consecutive renders that continued the previous one
     uint64_t frame_launches = 0;      // renders run as one persistent launch (pt_frame.hip)
     uint32_t pipe_next_seed = 0;      // random_seed of the render that would continue the last one
@@ -817,7 +818,7 @@ int render_pipelined(RenderCtx &cx, const FrameParams &fp, const pupil_pt_launch
         const uint32_t nring = ring_end();
         if (!pt->shade_list)  // material bins of every path traced in this iteration -> q.bins
             launch_partition(ring.mbin, nring, kPartMaxBins, kPartExclusive, 0u, q.bins, q.hist, q.counts,
-                             q.counts + kStartBins, q.counts + kScratch, nullptr, s);
+                             q.counts + kStartBins, q.counts + kScratch, nullptr, s, nullptr, nullptr, pt->bin_mask);
         FrameParams fs = fp;
         fs.group = G;  // AOV frame of a sample: its group frame (samples per ring slot = G spp)
         if (h.inject && h.nf.aov_scratch) {  // AOVs of frames ahead wait in their slot's scratch
@@ -1127,6 +1128,7 @@ int pupil_pt_create(const pupil_scene_desc *scene, int device, pupil_pt **out) {
             if (std::strcmp(sl, "list") == 0) pt->shade_list = true;
         }
         sc.single_bin = pt->shade_list && bins && (bins & (bins - 1u)) == 0u ? (uint32_t)__builtin_ctz(bins) : 0u;
+        pt->bin_mask = bins | 1u;  // the material bins a traced path can land in, and the miss bin
     }
     if (const char *fr = std::getenv("PUPIL_FRESH_SHADE")) pt->fresh_shade = std::atoi(fr) != 0;
     if (const char *a = std::getenv("PUPIL_AHEAD")) pt->ahead_mode = std::min(2, std::max(0, std::atoi(a)));

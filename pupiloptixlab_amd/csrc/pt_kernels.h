@@ -245,10 +245,13 @@ void launch_debug_select(const DeviceScene &sc, const float *p, int *out, uint32
 uint32_t partition_hist_entries(uint32_t n);
 // log_out (or null): the nbins counts; cum_out (or null): the counts are added to these
 // nbins running 64-bit totals (rays traced since the engine was created); snap_out (or
-// null): receives the totals as they were before this partition added to them
+// null): receives the totals as they were before this partition added to them; bin_mask (or 0 =
+// every bin below nbins): the bins a key can name -- the others are reported empty without being
+// ranked (the material partition of a scene with few materials)
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
                       uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, uint32_t *log_out,
-                      hipStream_t s, unsigned long long *cum_out = nullptr, unsigned long long *snap_out = nullptr);
+                      hipStream_t s, unsigned long long *cum_out = nullptr, unsigned long long *snap_out = nullptr,
+                      uint32_t bin_mask = 0u);
 
 // LBVH builder (bvh_build.hip)
 struct BvhBuildInput {

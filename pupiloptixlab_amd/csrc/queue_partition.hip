@@ -79,7 +79,7 @@ __device__ __forceinline__ void load_keys(const uint8_t *keys, uint32_t n, uint3
 }
 
 template <int MODE>
-__device__ __forceinline__ void count_wave(const uint8_t *keys, uint32_t n, uint32_t nbins, uint32_t shift,
+__device__ __forceinline__ void count_wave(const uint8_t *keys, uint32_t n, uint32_t bin_mask, uint32_t shift,
                                            uint32_t base, uint32_t rounds, uint32_t cnt[kPartMaxBins]) {
 #pragma unroll
     for (int b = 0; b < kPartMaxBins; b++) cnt[b] = 0;
@@ -90,19 +90,19 @@ __device__ __forceinline__ void count_wave(const uint8_t *keys, uint32_t n, uint
         for (uint32_t j = 0; j < kPartBatch; j++)
 #pragma unroll
             for (int b = 0; b < kPartMaxBins; b++)
-                if ((uint32_t)b < nbins)
+                if ((bin_mask >> b) & 1u)
                     cnt[b] += (uint32_t)__popcll(__ballot(in_bin<MODE>(k[j], (uint32_t)b, shift)));
     }
 }
 
 template <int MODE>
 __global__ __launch_bounds__(kPartBlock) void k_part_count(const uint8_t *keys, uint32_t n, uint32_t nbins,
-                                                           uint32_t shift, uint32_t *hist, uint32_t nblk,
-                                                           uint32_t rounds) {
+                                                           uint32_t bin_mask, uint32_t shift, uint32_t *hist,
+                                                           uint32_t nblk, uint32_t rounds) {
     __shared__ uint32_t s[4][kPartMaxBins];
     const uint32_t wave = threadIdx.x >> 6;
     uint32_t cnt[kPartMaxBins];
-    count_wave<MODE>(keys, n, nbins, shift, (blockIdx.x * 4u + wave) * 64u * rounds, rounds, cnt);
+    count_wave<MODE>(keys, n, bin_mask, shift, (blockIdx.x * 4u + wave) * 64u * rounds, rounds, cnt);
     if (__lane_id() == 0)
         for (int b = 0; b < kPartMaxBins; b++) s[wave][b] = cnt[b];
     __syncthreads();
@@ -188,20 +188,20 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t nbl
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys, uint32_t n, uint32_t nbins,
+__global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys, uint32_t n, uint32_t bin_mask,
                                                              uint32_t shift, const uint32_t *hist, uint32_t nblk,
                                                              uint32_t *out, uint32_t rounds) {
     __shared__ uint32_t s[4][kPartMaxBins];
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t base = (blockIdx.x * 4u + wave) * 64u * rounds;
     uint32_t off[kPartMaxBins];
-    count_wave<MODE>(keys, n, nbins, shift, base, rounds, off);
+    count_wave<MODE>(keys, n, bin_mask, shift, base, rounds, off);
     if (__lane_id() == 0)
         for (int b = 0; b < kPartMaxBins; b++) s[wave][b] = off[b];
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < kPartMaxBins; b++) {
-        if ((uint32_t)b >= nbins) continue;
+        if (!((bin_mask >> b) & 1u)) continue;
         uint32_t o = hist[b * nblk + blockIdx.x];
         for (uint32_t w = 0; w < wave; w++) o += s[w][b];
         off[b] = o;
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(const uint8_t *keys
             const uint32_t i = base + (r0 + j) * 64u + __lane_id();
 #pragma unroll
             for (int b = 0; b < kPartMaxBins; b++) {
-                if ((uint32_t)b >= nbins) continue;
+                if (!((bin_mask >> b) & 1u)) continue;
                 const bool mine = in_bin<MODE>(k[j], (uint32_t)b, shift);  // no_key past n / rounds: in no bin
                 const unsigned long long m = __ballot(mine);
                 if (mine) out[off[b] + (uint32_t)__popcll(m & lanes_below())] = i;
@@ -234,7 +234,10 @@ uint32_t partition_hist_entries(uint32_t n) {
 
 void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode mode, uint32_t shift, uint32_t *out,
                       uint32_t *hist, uint32_t *counts_out, uint32_t *starts_out, uint32_t *total_out, uint32_t *log_out,
-                      hipStream_t s, unsigned long long *cum_out, unsigned long long *snap_out) {
+                      hipStream_t s, unsigned long long *cum_out, unsigned long long *snap_out, uint32_t bin_mask) {
+    // the bins a key can name (the others are counted as empty without a ballot each)
+    const uint32_t all = (1u << nbins) - 1u;
+    bin_mask = bin_mask ? (bin_mask & all) : all;
     const uint32_t nblk = part_blocks(n);
     const uint32_t rounds = part_rounds(n);
     if (nblk == 0) {
@@ -247,12 +250,12 @@ void launch_partition(const uint8_t *keys, uint32_t n, uint32_t nbins, PartMode 
         return;
     }
 #define PART_RUN(M)                                                                                                \
-    hipLaunchKernelGGL(k_part_count<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk,      \
-                       rounds);                                                                                    \
+    hipLaunchKernelGGL(k_part_count<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, bin_mask, shift, hist, \
+                       nblk, rounds);                                                                                    \
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, hist, nblk, nbins, counts_out, starts_out,          \
                        total_out, log_out, cum_out, snap_out);                                                                      \
-    hipLaunchKernelGGL(k_part_scatter<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, nbins, shift, hist, nblk, out, \
-                       rounds)
+    hipLaunchKernelGGL(k_part_scatter<M>, dim3(nblk), dim3(kPartBlock), 0, s, keys, n, bin_mask, shift, hist, nblk, \
+                       out, rounds)
     switch (mode) {
     case kPartExclusive: PART_RUN(kPartExclusive); break;
     case kPartFlags: PART_RUN(kPartFlags); break;
