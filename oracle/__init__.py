@@ -52,6 +52,8 @@ def lib():
         L.oracle_camera_ray.argtypes = [vp, C.c_uint32, C.c_uint32, f32p]
         L.oracle_closest.argtypes = [vp, C.c_uint32, f32p, f32p, C.c_int]
         L.oracle_bsdf.argtypes = [vp, C.c_uint32, C.c_float, C.c_float, f32p, f32p, C.c_uint32, f32p]
+        L.oracle_emitter_sample.argtypes = [vp, C.c_uint32, f32p, f32p, C.c_float, C.c_float, f32p]
+        L.oracle_emitter_sample.restype = C.c_int
         L.oracle_math.argtypes = [C.c_uint32, f32p, f32p, f32p]
         L.oracle_num_prims.restype = C.c_uint32
         L.oracle_num_prims.argtypes = [vp]
@@ -128,6 +130,15 @@ class OracleScene:
         wo = np.ascontiguousarray(wo, np.float32)
         wi = np.ascontiguousarray(wi_eval, np.float32)
         lib().oracle_bsdf(self._h, material, uv[0], uv[1], _fp(wo), _fp(wi), seed, _fp(out))
+        return out
+
+    def emitter_sample(self, emitter, pos, nrm, xi):
+        """One SampleDirect of area emitter `emitter` from (pos, nrm): wi(3), pdf, distance, radiance(3)."""
+        out = np.zeros(8, np.float32)
+        p = np.ascontiguousarray(pos, np.float32)
+        n = np.ascontiguousarray(nrm, np.float32)
+        if lib().oracle_emitter_sample(self._h, emitter, _fp(p), _fp(n), float(xi[0]), float(xi[1]), _fp(out)) != 0:
+            raise ValueError("no such emitter")
         return out
 
     @property

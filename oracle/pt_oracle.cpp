@@ -1889,6 +1889,26 @@ void oracle_bsdf(oracle_scene *s, uint32_t material, float u, float v, const flo
     out[11] = ev.pdf;
 }
 
+// one SampleDirect of area emitter `emitter` (env when emitter == num areas) from a shading point
+// (emitter.h / area.h / sphere.h / env.h): out = wi(3), pdf, distance, radiance(3)
+int oracle_emitter_sample(oracle_scene *s, uint32_t emitter, const float *pos, const float *nrm, float x0, float x1,
+                          float *out) {
+    auto &sc = *reinterpret_cast<oracle::Scene *>(s);
+    using namespace oracle;
+    const Emitter *e = emitter < sc.emitters.areas.size() ? &sc.emitters.areas[emitter] : sc.emitters.env;
+    if (!e) return -1;
+    LocalGeometry g;
+    g.position = make_float3(pos[0], pos[1], pos[2]);
+    g.normal = make_float3(nrm[0], nrm[1], nrm[2]);
+    EmitterSampleRecord r;
+    e->SampleDirect(r, g, make_float2(x0, x1));
+    out[0] = r.wi.x, out[1] = r.wi.y, out[2] = r.wi.z;
+    out[3] = r.pdf;
+    out[4] = r.distance;
+    out[5] = r.radiance.x, out[6] = r.radiance.y, out[7] = r.radiance.z;
+    return 0;
+}
+
 // host evaluation of the probe pupil_debug_math runs on the device
 void oracle_math(uint32_t n, const float *x, const float *y2, float *out) {
     for (uint32_t i = 0; i < n; i++) {
