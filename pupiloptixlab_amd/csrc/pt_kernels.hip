@@ -38,9 +38,11 @@ __global__ __launch_bounds__(kShadeBlock) void k_generate(DeviceScene sc, FrameP
     if (p >= fp.num_paths) return;
     vec3 dir;
     const uint32_t rng = fresh_path(sc, fp, p, fp.seed0, dir);
-    st_ps(ps.ray_o + p, f4(camera_origin(sc.camera), 0.f));
     st_ps(ps.ray_d + p, make_float4(dir.x, dir.y, dir.z, 0.f));
+    // a camera ray's origin is the camera's: the traversal and a fresh path's shade take it from
+    // the scene (camera_origin), so only full records, read by stages that cannot tell, store it
     if (!full) return;
+    st_ps(ps.ray_o + p, f4(camera_origin(sc.camera), 0.f));
     st_ps(ps.thr + p, make_float4(1.f, 1.f, 1.f, 0.f));
     st_ps(ps.rad + p, make_float4(0.f, 0.f, 0.f, 0.f));
     st_ps(ps.misc + p, make_uint4(rng, 0u, 0u, 0u));

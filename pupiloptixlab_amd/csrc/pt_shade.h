@@ -41,7 +41,6 @@ __device__ __forceinline__ uint32_t camera_path(const Camera &cam, uint32_t widt
                        dot(v4(c[8], c[9], c[10], c[11]), d)));
     return rng;
 }
-__device__ __forceinline__ vec3 camera_origin(const Camera &cam) { return v3(cam.c2w[3], cam.c2w[7], cam.c2w[11]); }
 
 
 // ------------------------------------------------------------------ generate
@@ -78,8 +77,8 @@ struct HitGeo {
 // shading record (bvh_build.hip k_attrs: object-space vertices, normals, uvs).
 // ro_rec: the ray origin record, read only for a sphere hit (the triangle position is
 // interpolated from the vertices)
-__device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, const float4 *ro_rec, vec3 rd,
-                                             vec2 stale_uv) {
+__device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, const float4 *ro_rec, bool fresh,
+                                             vec3 rd, vec2 stale_uv) {
     HitGeo out;
     const uint32_t idx = __float_as_uint(h.w);
     // flat: idx = record in traversal order, which names the instance; two-level:
@@ -117,7 +116,8 @@ __device__ __forceinline__ HitGeo reconstruct(const DeviceScene &sc, float4 h, c
     g.texcoord = stale_uv;
     uint32_t local = 0;
     if (sphere) {
-        const vec3 ro = f3(ld_ps(ro_rec));
+        // a fresh path's ray is a camera ray, whose origin k_generate does not store
+        const vec3 ro = fresh ? camera_origin(sc.camera) : f3(ld_ps(ro_rec));
         g.position = ro + h.x * rd;
         const vec3 local_pos = xform_point(in.to_object, g.position);
         g.texcoord = sphere_texcoord(normalize(local_pos - v3(0.f)));
@@ -227,7 +227,7 @@ __device__ __forceinline__ uint32_t shade_hit(const DeviceScene &sc, const Frame
     vec3 L_add = v3(0.f);
     const vec2 stale_uv = v2(__uint_as_float(misc.z), __uint_as_float(misc.w));
 
-    HitGeo hg = reconstruct(sc, h, ps.ray_o + p, ray_d, stale_uv);
+    HitGeo hg = reconstruct(sc, h, ps.ray_o + p, fresh, ray_d, stale_uv);
     const DevInstance &in = sc.instances[hg.inst];
     const DevMaterial &mat = sc.materials[in.material];
     if (mat.twosided && dot(-ray_d, hg.g.normal) < 0.f) hg.g.normal = -hg.g.normal;  // geometry.h:316-320
@@ -361,7 +361,8 @@ __device__ __forceinline__ void shade_miss(const DeviceScene &sc, const FramePar
         if (sc.has_env) {
             vec3 Le;
             float pdf;
-            env_eval(*sc.env, f3(ld_ps(ps.ray_o + p)), f3(ld_ps(ps.ray_d + p)), Le, pdf);
+            const vec3 ro = fresh ? camera_origin(sc.camera) : f3(ld_ps(ps.ray_o + p));  // fresh: not stored
+            env_eval(*sc.env, ro, f3(ld_ps(ps.ray_d + p)), Le, pdf);
             L = L + Le;  // main.cu:185, no MIS on the camera ray
         }
         const float test = rng_next(rng);

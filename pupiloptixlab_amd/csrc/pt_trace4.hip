@@ -185,7 +185,8 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                     float4 o, d;
                     if (MODE == kModeExtend) {
                         p = job.queue ? job.queue[i] : (job.spp ? (i % job.spp) * job.num_local + i / job.spp : i);
-                        o = ld_ps(ps.ray_o + p);
+                        // no queue: the camera rays of a render (origin = the camera's, k_generate)
+                        o = job.queue ? ld_ps(ps.ray_o + p) : f4(camera_origin(sc.camera), 0.f);
                         d = ld_ps(ps.ray_d + p);
                         tmin = 0.001f;
                         tmax = kMaxDistance;
@@ -195,7 +196,7 @@ __device__ __forceinline__ void trace4_body(const DeviceScene &sc, const PathSta
                         const uint32_t j = lo_a + k;
                         p = (job.spp ? (j % job.spp) * job.num_local + j / job.spp : j) + job.ahead_base;
                         any = false;
-                        o = ld_ps(ps.ray_o + p);
+                        o = f4(camera_origin(sc.camera), 0.f);  // a camera ray (k_generate)
                         d = ld_ps(ps.ray_d + p);
                         tmin = 0.001f;
                         tmax = kMaxDistance;

@@ -18,6 +18,8 @@ __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << la
 
 __device__ __forceinline__ vec3 f3(float4 v) { return v3(v.x, v.y, v.z); }
 __device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
+// every camera ray's origin (main.cu:53-75: the camera-to-world translation)
+__device__ __forceinline__ vec3 camera_origin(const Camera &cam) { return v3(cam.c2w[3], cam.c2w[7], cam.c2w[11]); }
 
 // Leaf intersection (flattened BVH4 and two-level world mode).  any = terminate on the first
 // hit (shadow ray); a compile-time constant except in the mixed persistent kernel.
